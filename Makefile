@@ -1,0 +1,89 @@
+# Build for the SDA MI355X framework.
+#
+#   make            -> host core library, pybind11 modules, CLI binaries, HIP module
+#   make host       -> everything except the HIP (gfx950) extension
+#   make asan       -> AddressSanitizer/UBSan build of the host test binary
+#
+# Outputs (in-tree, git-ignored, shipped to the GPU box with the snapshot):
+#   sda_amd/_lib/_sda_native<EXT>   host control plane + crypto bindings
+#   sda_amd/_lib/_sda_gpu<EXT>      HIP/CDNA4 kernels (hipcc --offload-arch=gfx950)
+#   sda_amd/_lib/bin/sda, sdad      agent CLI and server daemon
+
+PYTHON   ?= python3
+CXX      ?= g++
+HIPCC    ?= /opt/rocm/bin/hipcc
+GPU_ARCH ?= gfx950
+
+EXT        := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+PY_INC     := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
+PYBIND_INC := $(shell $(PYTHON) -c "import pybind11;print(pybind11.get_include())")
+
+BUILD := build
+LIB   := sda_amd/_lib
+BIN   := $(LIB)/bin
+
+CXXFLAGS ?= -O3 -g -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -pthread
+INCS     := -Icsrc/include
+HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(GPU_ARCH) -Wall -Wno-unused-parameter \
+            -Wno-unused-result -munsafe-fp-atomics
+
+CORE_SRC := $(wildcard csrc/src/*.cc)
+CORE_OBJ := $(patsubst csrc/src/%.cc,$(BUILD)/core/%.o,$(CORE_SRC))
+CORE_LIB := $(BUILD)/libsdacore.a
+
+PY_SRC   := $(wildcard csrc/python/*.cc)
+PY_OBJ   := $(patsubst csrc/python/%.cc,$(BUILD)/py/%.o,$(PY_SRC))
+
+HIP_SRC  := $(wildcard csrc/kernels/*.hip)
+HIP_OBJ  := $(patsubst csrc/kernels/%.hip,$(BUILD)/hip/%.o,$(HIP_SRC))
+HIP_BIND := csrc/kernels/gpu_module.cpp
+
+NATIVE_MOD := $(LIB)/_sda_native$(EXT)
+GPU_MOD    := $(LIB)/_sda_gpu$(EXT)
+BINS       := $(patsubst csrc/bin/%.cc,$(BIN)/%,$(filter-out csrc/bin/sda_selftest.cc,$(wildcard csrc/bin/*.cc)))
+
+.PHONY: all host gpu clean asan
+all: host gpu
+host: $(NATIVE_MOD) $(BINS)
+gpu: $(GPU_MOD)
+
+$(BUILD)/core/%.o: csrc/src/%.cc $(wildcard csrc/include/sda/*.hpp)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) $(INCS) -c $< -o $@
+
+$(CORE_LIB): $(CORE_OBJ)
+	@mkdir -p $(dir $@)
+	rm -f $@ && ar rcs $@ $^
+
+$(BUILD)/py/%.o: csrc/python/%.cc $(wildcard csrc/include/sda/*.hpp)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -fvisibility=hidden $(INCS) -I$(PY_INC) -I$(PYBIND_INC) -c $< -o $@
+
+$(NATIVE_MOD): $(PY_OBJ) $(CORE_LIB)
+	@mkdir -p $(dir $@)
+	$(CXX) -shared -o $@ $(PY_OBJ) $(CORE_LIB) -pthread
+
+$(BIN)/%: csrc/bin/%.cc $(CORE_LIB)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) $(INCS) $< $(CORE_LIB) -o $@ -pthread
+
+$(BUILD)/hip/%.o: csrc/kernels/%.hip $(wildcard csrc/kernels/*.hpp) $(wildcard csrc/include/sda/*.hpp)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) $(INCS) -c $< -o $@
+
+$(BUILD)/hip/gpu_module.o: $(HIP_BIND) $(wildcard csrc/kernels/*.hpp) $(wildcard csrc/include/sda/*.hpp)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -O3 -std=c++17 -fPIC -fvisibility=hidden $(INCS) -I$(PY_INC) -I$(PYBIND_INC) -c $< -o $@
+
+$(GPU_MOD): $(HIP_OBJ) $(BUILD)/hip/gpu_module.o $(CORE_LIB)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -shared --offload-arch=$(GPU_ARCH) -o $@ $^ -pthread
+
+asan:
+	@mkdir -p $(BUILD)/asan
+	$(CXX) -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer $(INCS) \
+	    csrc/bin/sda_selftest.cc $(CORE_SRC) -o $(BUILD)/asan/sda_selftest -pthread
+	$(BUILD)/asan/sda_selftest
+
+clean:
+	rm -rf $(BUILD) $(LIB)/*.so $(BIN)

@@ -1,0 +1,161 @@
+#!/usr/bin/env python3
+"""Headline benchmark: aggregated secret-shared elements/sec.
+
+BASELINE.json metric: "aggregated secret-shared elements/sec (1M-dim vec, 1k
+participants, 3 clerks)" -- config 2: 1000 participants x 1,000,000-dim vectors,
+3-way additive sharing mod 433, no mask, libsodium-compatible sealed boxes.
+
+One *step* is a complete SDA round, end to end on device: participants mask +
+share + seal (X25519 / XSalsa20-Poly1305) their vectors for every clerk, shares
+are routed to the clerks, every clerk verifies + decrypts + decodes + combines
+its P boxes and seals the sum for the recipient, the recipient opens the n
+results, reconstructs and unmasks. elements/s = participants x dimension / step
+time (whole job: summed over all ranks).
+
+Scaling is *weak*: each rank hosts `--participants` (default 1000) participants,
+so N ranks aggregate N x 1000 x 1M elements per step. With N > 1 the round runs
+through sda_amd.parallel (RCCL all-to-all of the sealed boxes over xGMI,
+clerk partials reduced to the clerks' lead ranks, results gathered to rank 0).
+
+Launch: python bench.py --gpus 1 --steps 5 --warmup 2
+        python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+            --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "aggregated secret-shared elements/sec (1M-dim vec, 1k participants, 3 clerks)"
+# Reference-equivalent single-threaded CPU implementation measured here (the
+# reference publishes no numbers). None until recorded.
+BASELINE_ELEMS_PER_S = None
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--participants", type=int, default=1000, help="participants per rank")
+    ap.add_argument("--dim", type=int, default=1_000_000)
+    ap.add_argument("--clerks", type=int, default=3)
+    ap.add_argument("--modulus", type=int, default=433)
+    ap.add_argument("--check", action="store_true", help="verify the output every step")
+    ap.add_argument("--stages", action="store_true", help="print per-stage times (rank 0)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("bench.py: launch with torch.distributed.run for --gpus > 1", file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from sda_amd.models.schemes import Additive, AggregationSpec, NoMask
+
+    spec = AggregationSpec(args.dim, args.modulus, Additive(args.clerks, args.modulus), NoMask(),
+                           title="bench")
+    P = args.participants
+    gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    secrets = torch.randint(0, args.modulus, (P, args.dim), dtype=torch.int32, device="cuda",
+                            generator=gen)
+
+    if world == 1:
+        from sda_amd.engine import DeviceAggregator, reference_sum
+
+        agg = DeviceAggregator(spec, time_stages=args.stages)
+
+        def step(check):
+            res = agg.run_round(secrets, check=check)
+            return res
+
+        expected = reference_sum(secrets, args.modulus) if args.check else None
+    else:
+        from sda_amd.parallel.engine import DistributedAggregator
+
+        agg = DistributedAggregator(spec, participants_per_rank=P, time_stages=args.stages)
+
+        def step(check):
+            return agg.run_round(secrets, check=check)
+
+        expected = None
+
+    # warmup (also validates the result once)
+    for i in range(args.warmup):
+        res = step(check=True)
+        if i == 0 and world == 1:
+            ref = reference_sum(secrets, args.modulus)
+            if not torch.equal(res.output, ref):
+                raise SystemExit("bench: device aggregation does not match the reference sum")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step(check=args.check)
+        if expected is not None and not torch.equal(res.output, expected):
+            raise SystemExit("bench: mismatch")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+    total_elems = P * world * args.dim
+    value = total_elems / (ms / 1e3)
+    if rank == 0:
+        if args.stages and getattr(res, "stage_ms", None):
+            print(json.dumps({"stage_ms": res.stage_ms}), file=sys.stderr)
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "elements/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (value / BASELINE_ELEMS_PER_S) if BASELINE_ELEMS_PER_S else None,
+            "dtype": "int32 (field elements mod 433; no floating point in this workload)",
+            "data": "synthetic uniform random participant vectors in [0, 433)",
+            "config": {
+                "model": f"SDA round: additive-{args.clerks} sharing, mod {args.modulus}, no mask, "
+                         "libsodium sealed boxes (X25519+XSalsa20-Poly1305), zigzag varint",
+                "global_batch": P * world,
+                "seq_len": args.dim,
+                "participants_per_gpu": P,
+                "dimension": args.dim,
+                "clerks": args.clerks,
+                "parallelism": f"participants sharded x{world}, clerk jobs all-to-all" if world > 1
+                               else "single GPU",
+            },
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,508 @@
+// Device-side (gfx950) cryptographic building blocks.
+//
+// Everything here runs on 32-bit VALU lanes of a 64-wide wavefront:
+//  * Salsa20 / HSalsa20 / ChaCha20 cores (ARX; rotates lower to v_alignbit_b32)
+//  * BLAKE2b single-block compression (sealed-box nonce, libsodium
+//    crypto_box_seal_nonce)
+//  * Poly1305 in 5 x 26-bit limbs (32x32->64 products -> v_mad_u64_u32)
+//  * GF(2^255-19) in 8 x 32-bit limbs for the X25519 Montgomery ladder
+//
+// Bit-exactness against the host oracle (csrc/src/crypto_*.cc) is covered by
+// tests/test_gpu_kernels.py.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#define SDA_DEV __device__ __forceinline__
+
+namespace sdagpu {
+
+SDA_DEV uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+SDA_DEV uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+constexpr uint32_t kSigma0 = 0x61707865u, kSigma1 = 0x3320646eu, kSigma2 = 0x79622d32u,
+                   kSigma3 = 0x6b206574u;
+
+// ---------------------------------------------------------------- Salsa20 ---
+SDA_DEV void salsa20_rounds(uint32_t (&x)[16]) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    x[4] ^= rotl32(x[0] + x[12], 7);   x[8] ^= rotl32(x[4] + x[0], 9);
+    x[12] ^= rotl32(x[8] + x[4], 13);  x[0] ^= rotl32(x[12] + x[8], 18);
+    x[9] ^= rotl32(x[5] + x[1], 7);    x[13] ^= rotl32(x[9] + x[5], 9);
+    x[1] ^= rotl32(x[13] + x[9], 13);  x[5] ^= rotl32(x[1] + x[13], 18);
+    x[14] ^= rotl32(x[10] + x[6], 7);  x[2] ^= rotl32(x[14] + x[10], 9);
+    x[6] ^= rotl32(x[2] + x[14], 13);  x[10] ^= rotl32(x[6] + x[2], 18);
+    x[3] ^= rotl32(x[15] + x[11], 7);  x[7] ^= rotl32(x[3] + x[15], 9);
+    x[11] ^= rotl32(x[7] + x[3], 13);  x[15] ^= rotl32(x[11] + x[7], 18);
+    x[1] ^= rotl32(x[0] + x[3], 7);    x[2] ^= rotl32(x[1] + x[0], 9);
+    x[3] ^= rotl32(x[2] + x[1], 13);   x[0] ^= rotl32(x[3] + x[2], 18);
+    x[6] ^= rotl32(x[5] + x[4], 7);    x[7] ^= rotl32(x[6] + x[5], 9);
+    x[4] ^= rotl32(x[7] + x[6], 13);   x[5] ^= rotl32(x[4] + x[7], 18);
+    x[11] ^= rotl32(x[10] + x[9], 7);  x[8] ^= rotl32(x[11] + x[10], 9);
+    x[9] ^= rotl32(x[8] + x[11], 13);  x[10] ^= rotl32(x[9] + x[8], 18);
+    x[12] ^= rotl32(x[15] + x[14], 7); x[13] ^= rotl32(x[12] + x[15], 9);
+    x[14] ^= rotl32(x[13] + x[12], 13); x[15] ^= rotl32(x[14] + x[13], 18);
+  }
+}
+
+// 64-byte Salsa20/20 block as 16 little-endian words.
+SDA_DEV void salsa20_block(uint32_t (&out)[16], const uint32_t (&k)[8], uint32_t n0, uint32_t n1,
+                           uint64_t ctr) {
+  uint32_t j[16] = {kSigma0, k[0], k[1], k[2], k[3], kSigma1, n0, n1,
+                    (uint32_t)ctr, (uint32_t)(ctr >> 32), kSigma2, k[4], k[5], k[6], k[7], kSigma3};
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = j[i];
+  salsa20_rounds(x);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) out[i] = x[i] + j[i];
+}
+
+SDA_DEV void hsalsa20(uint32_t (&out)[8], const uint32_t (&k)[8], const uint32_t (&in)[4]) {
+  uint32_t x[16] = {kSigma0, k[0], k[1], k[2], k[3], kSigma1, in[0], in[1],
+                    in[2],   in[3], kSigma2, k[4], k[5], k[6], k[7], kSigma3};
+  salsa20_rounds(x);
+  out[0] = x[0]; out[1] = x[5]; out[2] = x[10]; out[3] = x[15];
+  out[4] = x[6]; out[5] = x[7]; out[6] = x[8]; out[7] = x[9];
+}
+
+// ---------------------------------------------------------------- ChaCha20 --
+#define SDA_CHACHA_QR(a, b, c, d)            \
+  a += b; d ^= a; d = rotl32(d, 16);         \
+  c += d; b ^= c; b = rotl32(b, 12);         \
+  a += b; d ^= a; d = rotl32(d, 8);          \
+  c += d; b ^= c; b = rotl32(b, 7);
+
+template <int ROUNDS = 20>
+SDA_DEV void chacha_block(uint32_t (&out)[16], const uint32_t (&in)[16]) {
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = in[i];
+#pragma unroll
+  for (int i = 0; i < ROUNDS; i += 2) {
+    SDA_CHACHA_QR(x[0], x[4], x[8], x[12]);
+    SDA_CHACHA_QR(x[1], x[5], x[9], x[13]);
+    SDA_CHACHA_QR(x[2], x[6], x[10], x[14]);
+    SDA_CHACHA_QR(x[3], x[7], x[11], x[15]);
+    SDA_CHACHA_QR(x[0], x[5], x[10], x[15]);
+    SDA_CHACHA_QR(x[1], x[6], x[11], x[12]);
+    SDA_CHACHA_QR(x[2], x[7], x[8], x[13]);
+    SDA_CHACHA_QR(x[3], x[4], x[9], x[14]);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) out[i] = x[i] + in[i];
+}
+
+// Counter-mode device CSPRNG: ChaCha20(key, counter = block, nonce = stream id).
+// State words 12..13 = 64-bit block counter, 14..15 = 64-bit stream id.
+struct RngKey {
+  uint32_t k[8];
+};
+SDA_DEV void rng_block(uint32_t (&out)[16], const RngKey& key, uint64_t stream, uint64_t block) {
+  uint32_t in[16] = {kSigma0, kSigma1, kSigma2, kSigma3, key.k[0], key.k[1], key.k[2], key.k[3],
+                     key.k[4], key.k[5], key.k[6], key.k[7], (uint32_t)block,
+                     (uint32_t)(block >> 32), (uint32_t)stream, (uint32_t)(stream >> 32)};
+  chacha_block<20>(out, in);
+}
+
+// Stream ids: purpose in the top byte, then the owner index.
+enum RngPurpose : uint64_t {
+  kPurposeShares = 1,
+  kPurposeSharesRetry = 2,
+  kPurposeMaskFull = 3,
+  kPurposeMaskRetry = 4,
+  kPurposeChaChaSeed = 5,
+  kPurposeEphemeral = 6,
+};
+SDA_DEV uint64_t stream_id(uint64_t purpose, uint64_t owner) { return (purpose << 56) | owner; }
+
+// Exact uniform draw in [0, m) for one (stream, draw index): the primary word is
+// word `idx` of the stream; a rejected word falls back to a private retry stream
+// keyed by (owner, idx) so the result stays a pure function of (stream, idx).
+SDA_DEV uint32_t uniform_fixup(const RngKey& key, uint64_t retry_purpose, uint64_t owner,
+                               uint64_t idx, uint32_t m, uint32_t zone) {
+  // retry stream: owner in the stream id, (idx) as block counter high bits
+  for (uint64_t blk = 0;; ++blk) {
+    uint32_t w[16];
+    rng_block(w, key, stream_id(retry_purpose, owner), (idx << 8) | blk);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (w[i] < zone) return w[i] % m;
+  }
+}
+
+// ---------------------------------------------------------------- BLAKE2b ---
+// BLAKE2b-192 of a 64-byte message given as 16 LE words (libsodium seal nonce).
+SDA_DEV void blake2b_192_64(uint32_t (&out)[6], const uint32_t (&msg)[16]) {
+  const uint64_t IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                          0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                          0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  const uint8_t S[12][16] = {
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+      {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+      {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+      {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+      {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+      {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+      {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+      {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+      {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+      {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+      {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+  uint64_t m[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m[i] = (uint64_t)msg[2 * i] | ((uint64_t)msg[2 * i + 1] << 32);
+#pragma unroll
+  for (int i = 8; i < 16; ++i) m[i] = 0;
+  uint64_t h[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h[i] = IV[i];
+  h[0] ^= 0x01010000ULL ^ 24ULL;
+  uint64_t v[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { v[i] = h[i]; v[i + 8] = IV[i]; }
+  v[12] ^= 64ULL;  // t0 = 64 bytes
+  v[14] = ~v[14];  // last block
+#define SDA_B2G(a, b, c, d, x, y)                    \
+  v[a] = v[a] + v[b] + (x); v[d] = rotr64(v[d] ^ v[a], 32); \
+  v[c] = v[c] + v[d];       v[b] = rotr64(v[b] ^ v[c], 24); \
+  v[a] = v[a] + v[b] + (y); v[d] = rotr64(v[d] ^ v[a], 16); \
+  v[c] = v[c] + v[d];       v[b] = rotr64(v[b] ^ v[c], 63);
+#pragma unroll
+  for (int r = 0; r < 12; ++r) {
+    SDA_B2G(0, 4, 8, 12, m[S[r][0]], m[S[r][1]]);
+    SDA_B2G(1, 5, 9, 13, m[S[r][2]], m[S[r][3]]);
+    SDA_B2G(2, 6, 10, 14, m[S[r][4]], m[S[r][5]]);
+    SDA_B2G(3, 7, 11, 15, m[S[r][6]], m[S[r][7]]);
+    SDA_B2G(0, 5, 10, 15, m[S[r][8]], m[S[r][9]]);
+    SDA_B2G(1, 6, 11, 12, m[S[r][10]], m[S[r][11]]);
+    SDA_B2G(2, 7, 8, 13, m[S[r][12]], m[S[r][13]]);
+    SDA_B2G(3, 4, 9, 14, m[S[r][14]], m[S[r][15]]);
+  }
+#undef SDA_B2G
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    uint64_t hv = h[i] ^ v[i] ^ v[i + 8];
+    out[2 * i] = (uint32_t)hv;
+    out[2 * i + 1] = (uint32_t)(hv >> 32);
+  }
+}
+
+// --------------------------------------------------------------- Poly1305 ---
+struct P130 {
+  uint32_t v[5];
+};
+constexpr uint32_t kM26 = 0x3ffffff;
+
+SDA_DEV P130 p130_zero() { return P130{{0, 0, 0, 0, 0}}; }
+
+// Clamped r from the 16 key bytes (4 LE words).
+SDA_DEV P130 p130_r_from_key(const uint32_t (&k)[4]) {
+  P130 r;
+  r.v[0] = k[0] & 0x3ffffff;
+  r.v[1] = ((k[0] >> 26) | (k[1] << 6)) & 0x3ffff03;
+  r.v[2] = ((k[1] >> 20) | (k[2] << 12)) & 0x3ffc0ff;
+  r.v[3] = ((k[2] >> 14) | (k[3] << 18)) & 0x3f03fff;
+  r.v[4] = (k[3] >> 8) & 0x00fffff;
+  return r;
+}
+// 16-byte block (4 LE words) with the 2^128 (or pad) bit
+SDA_DEV P130 p130_block(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t hibit) {
+  P130 c;
+  c.v[0] = w0 & kM26;
+  c.v[1] = ((w0 >> 26) | (w1 << 6)) & kM26;
+  c.v[2] = ((w1 >> 20) | (w2 << 12)) & kM26;
+  c.v[3] = ((w2 >> 14) | (w3 << 18)) & kM26;
+  c.v[4] = (w3 >> 8) | hibit;
+  return c;
+}
+SDA_DEV P130 p130_add(const P130& a, const P130& b) {
+  P130 r;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) r.v[i] = a.v[i] + b.v[i];
+  return r;
+}
+// General product mod 2^130-5, operand limbs < 2^27; result limbs < 2^26 (limb1 < 2^27).
+SDA_DEV P130 p130_mul(const P130& h, const P130& r) {
+  const uint32_t s1 = r.v[1] * 5, s2 = r.v[2] * 5, s3 = r.v[3] * 5, s4 = r.v[4] * 5;
+  uint64_t d0 = (uint64_t)h.v[0] * r.v[0] + (uint64_t)h.v[1] * s4 + (uint64_t)h.v[2] * s3 +
+                (uint64_t)h.v[3] * s2 + (uint64_t)h.v[4] * s1;
+  uint64_t d1 = (uint64_t)h.v[0] * r.v[1] + (uint64_t)h.v[1] * r.v[0] + (uint64_t)h.v[2] * s4 +
+                (uint64_t)h.v[3] * s3 + (uint64_t)h.v[4] * s2;
+  uint64_t d2 = (uint64_t)h.v[0] * r.v[2] + (uint64_t)h.v[1] * r.v[1] + (uint64_t)h.v[2] * r.v[0] +
+                (uint64_t)h.v[3] * s4 + (uint64_t)h.v[4] * s3;
+  uint64_t d3 = (uint64_t)h.v[0] * r.v[3] + (uint64_t)h.v[1] * r.v[2] + (uint64_t)h.v[2] * r.v[1] +
+                (uint64_t)h.v[3] * r.v[0] + (uint64_t)h.v[4] * s4;
+  uint64_t d4 = (uint64_t)h.v[0] * r.v[4] + (uint64_t)h.v[1] * r.v[3] + (uint64_t)h.v[2] * r.v[2] +
+                (uint64_t)h.v[3] * r.v[1] + (uint64_t)h.v[4] * r.v[0];
+  P130 o;
+  uint64_t c;
+  c = d0 >> 26; o.v[0] = (uint32_t)d0 & kM26; d1 += c;
+  c = d1 >> 26; o.v[1] = (uint32_t)d1 & kM26; d2 += c;
+  c = d2 >> 26; o.v[2] = (uint32_t)d2 & kM26; d3 += c;
+  c = d3 >> 26; o.v[3] = (uint32_t)d3 & kM26; d4 += c;
+  c = d4 >> 26; o.v[4] = (uint32_t)d4 & kM26;
+  uint64_t t = (uint64_t)o.v[0] + c * 5;
+  o.v[0] = (uint32_t)t & kM26;
+  o.v[1] += (uint32_t)(t >> 26);
+  return o;
+}
+// Normalise limbs (< 2^26 each) after additions.
+SDA_DEV P130 p130_carry(P130 h) {
+  uint32_t c;
+  c = h.v[0] >> 26; h.v[0] &= kM26; h.v[1] += c;
+  c = h.v[1] >> 26; h.v[1] &= kM26; h.v[2] += c;
+  c = h.v[2] >> 26; h.v[2] &= kM26; h.v[3] += c;
+  c = h.v[3] >> 26; h.v[3] &= kM26; h.v[4] += c;
+  c = h.v[4] >> 26; h.v[4] &= kM26; h.v[0] += c * 5;
+  c = h.v[0] >> 26; h.v[0] &= kM26; h.v[1] += c;
+  return h;
+}
+SDA_DEV P130 p130_pow(P130 r, uint32_t e) {
+  P130 acc = P130{{1, 0, 0, 0, 0}};
+  while (e) {
+    if (e & 1) acc = p130_mul(acc, r);
+    r = p130_mul(r, r);
+    e >>= 1;
+  }
+  return acc;
+}
+// Final tag = (h mod p + s) mod 2^128, as 4 LE words.
+SDA_DEV void p130_finish(uint32_t (&tag)[4], P130 h, const uint32_t (&s)[4]) {
+  uint32_t h0 = h.v[0], h1 = h.v[1], h2 = h.v[2], h3 = h.v[3], h4 = h.v[4], c;
+  c = h0 >> 26; h0 &= kM26; h1 += c;
+  c = h1 >> 26; h1 &= kM26; h2 += c;
+  c = h2 >> 26; h2 &= kM26; h3 += c;
+  c = h3 >> 26; h3 &= kM26; h4 += c;
+  c = h4 >> 26; h4 &= kM26; h0 += c * 5;
+  c = h0 >> 26; h0 &= kM26; h1 += c;
+  c = h1 >> 26; h1 &= kM26; h2 += c;
+  uint32_t g0 = h0 + 5; c = g0 >> 26; g0 &= kM26;
+  uint32_t g1 = h1 + c; c = g1 >> 26; g1 &= kM26;
+  uint32_t g2 = h2 + c; c = g2 >> 26; g2 &= kM26;
+  uint32_t g3 = h3 + c; c = g3 >> 26; g3 &= kM26;
+  uint32_t g4 = h4 + c - (1u << 26);
+  uint32_t mask = (g4 >> 31) - 1;
+  g0 &= mask; g1 &= mask; g2 &= mask; g3 &= mask; g4 &= mask;
+  mask = ~mask;
+  h0 = (h0 & mask) | g0; h1 = (h1 & mask) | g1; h2 = (h2 & mask) | g2;
+  h3 = (h3 & mask) | g3; h4 = (h4 & mask) | g4;
+  uint32_t w0 = h0 | (h1 << 26);
+  uint32_t w1 = (h1 >> 6) | (h2 << 20);
+  uint32_t w2 = (h2 >> 12) | (h3 << 14);
+  uint32_t w3 = (h3 >> 18) | (h4 << 8);
+  uint64_t f;
+  f = (uint64_t)w0 + s[0]; tag[0] = (uint32_t)f;
+  f = (uint64_t)w1 + s[1] + (f >> 32); tag[1] = (uint32_t)f;
+  f = (uint64_t)w2 + s[2] + (f >> 32); tag[2] = (uint32_t)f;
+  f = (uint64_t)w3 + s[3] + (f >> 32); tag[3] = (uint32_t)f;
+}
+
+// -------------------------------------------------------- GF(2^255 - 19) ----
+struct Fe {
+  uint32_t v[8];
+};
+SDA_DEV Fe fe_set(uint32_t x) { return Fe{{x, 0, 0, 0, 0, 0, 0, 0}}; }
+
+SDA_DEV Fe fe_add(const Fe& a, const Fe& b) {
+  Fe r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { c += (uint64_t)a.v[i] + b.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
+  c *= 38;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
+  r.v[0] += (uint32_t)(c * 38);
+  return r;
+}
+SDA_DEV Fe fe_sub(const Fe& a, const Fe& b) {
+  Fe r;
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { c += (int64_t)a.v[i] - (int64_t)b.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
+  c *= 38;  // borrow -> subtract 38 (2^256 == 38)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
+  r.v[0] -= (uint32_t)((-c) * 38);
+  return r;
+}
+SDA_DEV Fe fe_reduce512(const uint32_t (&t)[16]) {
+  Fe r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (uint64_t)t[i] + (uint64_t)t[i + 8] * 38;
+    r.v[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  c *= 38;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
+  r.v[0] += (uint32_t)(c * 38);
+  return r;
+}
+SDA_DEV Fe fe_mul(const Fe& a, const Fe& b) {
+  uint32_t t[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      c += (uint64_t)a.v[i] * b.v[j] + t[i + j];
+      t[i + j] = (uint32_t)c;
+      c >>= 32;
+    }
+    t[i + 8] = (uint32_t)c;
+  }
+  return fe_reduce512(t);
+}
+SDA_DEV Fe fe_sq(const Fe& a) {
+  // off-diagonal products once, doubled, plus the diagonal
+  uint32_t t[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = i + 1; j < 8; ++j) {
+      c += (uint64_t)a.v[i] * a.v[j] + t[i + j];
+      t[i + j] = (uint32_t)c;
+      c >>= 32;
+    }
+    t[i + 8] = (uint32_t)c;
+  }
+  uint32_t top = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {  // double
+    uint32_t nt = t[i] >> 31;
+    t[i] = (t[i] << 1) | top;
+    top = nt;
+  }
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint64_t sq = (uint64_t)a.v[i] * a.v[i];
+    c += (uint64_t)t[2 * i] + (uint32_t)sq;
+    t[2 * i] = (uint32_t)c;
+    c >>= 32;
+    c += (uint64_t)t[2 * i + 1] + (uint32_t)(sq >> 32);
+    t[2 * i + 1] = (uint32_t)c;
+    c >>= 32;
+  }
+  return fe_reduce512(t);
+}
+SDA_DEV Fe fe_mul_small(const Fe& a, uint32_t s) {
+  Fe r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { c += (uint64_t)a.v[i] * s; r.v[i] = (uint32_t)c; c >>= 32; }
+  c *= 38;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
+  r.v[0] += (uint32_t)(c * 38);
+  return r;
+}
+SDA_DEV Fe fe_sqn(Fe a, int n) {
+  for (int i = 0; i < n; ++i) a = fe_sq(a);
+  return a;
+}
+SDA_DEV Fe fe_invert(const Fe& z) {
+  Fe z2 = fe_sq(z);
+  Fe z8 = fe_sqn(z2, 2);
+  Fe z9 = fe_mul(z8, z);
+  Fe z11 = fe_mul(z9, z2);
+  Fe z22 = fe_sq(z11);
+  Fe z_5_0 = fe_mul(z22, z9);
+  Fe z_10_0 = fe_mul(fe_sqn(z_5_0, 5), z_5_0);
+  Fe z_20_0 = fe_mul(fe_sqn(z_10_0, 10), z_10_0);
+  Fe z_40_0 = fe_mul(fe_sqn(z_20_0, 20), z_20_0);
+  Fe z_50_0 = fe_mul(fe_sqn(z_40_0, 10), z_10_0);
+  Fe z_100_0 = fe_mul(fe_sqn(z_50_0, 50), z_50_0);
+  Fe z_200_0 = fe_mul(fe_sqn(z_100_0, 100), z_100_0);
+  Fe z_250_0 = fe_mul(fe_sqn(z_200_0, 50), z_50_0);
+  return fe_mul(fe_sqn(z_250_0, 5), z11);
+}
+// Fully reduce to [0, p).
+SDA_DEV Fe fe_canon(Fe r) {
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    uint32_t top = r.v[7] >> 31;
+    r.v[7] &= 0x7fffffffu;
+    uint64_t c = (uint64_t)top * 19;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
+  }
+  // r < 2^255 + small; subtract p if r >= p  <=>  r + 19 >= 2^255
+  Fe t;
+  uint64_t c = 19;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { c += r.v[i]; t.v[i] = (uint32_t)c; c >>= 32; }
+  uint32_t ge = t.v[7] >> 31;
+  t.v[7] &= 0x7fffffffu;
+  uint32_t mask = 0u - ge;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = (r.v[i] & ~mask) | (t.v[i] & mask);
+  return r;
+}
+SDA_DEV void fe_cswap(Fe& a, Fe& b, uint32_t swap) {
+  uint32_t mask = 0u - swap;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint32_t t = mask & (a.v[i] ^ b.v[i]);
+    a.v[i] ^= t;
+    b.v[i] ^= t;
+  }
+}
+
+// X25519(scalar, u): RFC 7748 ladder. Words are little-endian.
+SDA_DEV void x25519(uint32_t (&out)[8], const uint32_t (&scalar)[8], const uint32_t (&u)[8]) {
+  uint32_t k[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) k[i] = scalar[i];
+  k[0] &= 0xfffffff8u;
+  k[7] &= 0x7fffffffu;
+  k[7] |= 0x40000000u;
+  Fe x1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x1.v[i] = u[i];
+  x1.v[7] &= 0x7fffffffu;
+  Fe x2 = fe_set(1), z2 = fe_set(0), x3 = x1, z3 = fe_set(1);
+  uint32_t swap = 0;
+  for (int t = 254; t >= 0; --t) {
+    uint32_t kt = (k[t >> 5] >> (t & 31)) & 1;
+    swap ^= kt;
+    fe_cswap(x2, x3, swap);
+    fe_cswap(z2, z3, swap);
+    swap = kt;
+    Fe A = fe_add(x2, z2), AA = fe_sq(A);
+    Fe B = fe_sub(x2, z2), BB = fe_sq(B);
+    Fe E = fe_sub(AA, BB);
+    Fe C = fe_add(x3, z3), D = fe_sub(x3, z3);
+    Fe DA = fe_mul(D, A), CB = fe_mul(C, B);
+    x3 = fe_sq(fe_add(DA, CB));
+    z3 = fe_mul(x1, fe_sq(fe_sub(DA, CB)));
+    x2 = fe_mul(AA, BB);
+    z2 = fe_mul(E, fe_add(AA, fe_mul_small(E, 121665)));
+  }
+  fe_cswap(x2, x3, swap);
+  fe_cswap(z2, z3, swap);
+  Fe r = fe_canon(fe_mul(x2, fe_invert(z2)));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out[i] = r.v[i];
+}
+
+// ------------------------------------------------------------------ varint --
+// zigzag(LEB128) length of a canonical value v in [0, 2^31): z = 2v.
+SDA_DEV uint32_t varint_len_canon(uint32_t v) {
+  uint32_t z = v << 1;
+  return 1u + (z >= (1u << 7)) + (z >= (1u << 14)) + (z >= (1u << 21)) + (z >= (1u << 28));
+}
+
+}  // namespace sdagpu

@@ -1,0 +1,170 @@
+// pybind11 bindings for the gfx950 kernels (`sda_amd._lib._sda_gpu`).
+//
+// Tensors cross the boundary as raw device pointers (tensor.data_ptr()) and the
+// current HIP stream as an integer handle; shape/dtype/device validation is done
+// in sda_amd/ops/gpu.py before any launch.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+
+namespace py = pybind11;
+using namespace sdagpu;
+
+namespace {
+
+template <typename T>
+T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+RngKeyArg rng_from(const std::vector<uint32_t>& k) {
+  if (k.size() != 8) throw std::invalid_argument("rng key must be 8 x u32");
+  RngKeyArg a;
+  for (int i = 0; i < 8; ++i) a.k[i] = k[i];
+  return a;
+}
+
+void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_sda_gpu, m) {
+  m.doc() = "SDA MI355X (gfx950) HIP kernels";
+  m.attr("TILE_VALUES") = kTileValues;
+  m.attr("CHUNK_BYTES") = kChunkBytes;
+  m.attr("MSGKEY_BYTES") = (int)sizeof(MsgKey);
+  m.attr("ERR_BAD_KEY") = (int)kErrBadKey;
+  m.attr("ERR_MAC") = (int)kErrMac;
+  m.attr("ERR_MALFORMED") = (int)kErrMalformed;
+  m.attr("ERR_CHACHA_REJECT") = (int)kErrChaChaReject;
+  m.attr("ERR_RANGE") = (int)kErrRange;
+
+  m.def("device_info", []() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) != hipSuccess) throw std::runtime_error("no HIP device");
+    py::dict d;
+    d["name"] = std::string(p.name);
+    d["gcn_arch"] = std::string(p.gcnArchName);
+    d["cus"] = p.multiProcessorCount;
+    d["lds_per_block"] = (long long)p.sharedMemPerBlock;
+    d["total_mem"] = (long long)p.totalGlobalMem;
+    return d;
+  });
+
+  m.def("seal_setup", [](int M, std::vector<uint32_t> rng, uint64_t owner_base, uintptr_t key_idx,
+                         uintptr_t pks, uintptr_t ct, uint64_t stride, uintptr_t keys,
+                         uintptr_t err, uintptr_t stream) {
+    launch_seal_setup(M, rng_from(rng), owner_base, P<const uint32_t>(key_idx),
+                      P<const uint32_t>(pks), P<uint8_t>(ct), stride, P<MsgKey>(keys),
+                      P<uint32_t>(err), S(stream));
+    check_launch("seal_setup");
+  });
+  m.def("open_setup", [](int M, uintptr_t key_idx, uintptr_t sks, uintptr_t pks, uintptr_t ct,
+                         uint64_t stride, uintptr_t keys, uintptr_t err, uintptr_t stream) {
+    launch_open_setup(M, P<const uint32_t>(key_idx), P<const uint32_t>(sks),
+                      P<const uint32_t>(pks), P<const uint8_t>(ct), stride, P<MsgKey>(keys),
+                      P<uint32_t>(err), S(stream));
+    check_launch("open_setup");
+  });
+  m.def("x25519", [](int N, uintptr_t sc, uintptr_t pt, uintptr_t out, uintptr_t stream) {
+    launch_x25519(N, P<const uint32_t>(sc), P<const uint32_t>(pt), P<uint32_t>(out), S(stream));
+    check_launch("x25519");
+  });
+  m.def("share_additive",
+        [](int Pn, int D, int n, uint32_t mod, int value_bytes, uintptr_t secrets, int mask_mode,
+           int seed_words, std::vector<uint32_t> rng, uint64_t owner_base, uintptr_t shares,
+           uintptr_t cnt, uintptr_t mask_out, uintptr_t mask_cnt, uintptr_t seeds, uintptr_t err,
+           uintptr_t stream) {
+          launch_share_additive(Pn, D, n, mod, value_bytes, P<const int32_t>(secrets), mask_mode,
+                                seed_words, rng_from(rng), owner_base, P<void>(shares),
+                                P<uint32_t>(cnt), P<uint32_t>(mask_out), P<uint32_t>(mask_cnt),
+                                P<uint32_t>(seeds), P<uint32_t>(err), S(stream));
+          check_launch("share_additive");
+        });
+  m.def("share_pss",
+        [](int Pn, int D, int n, int k, int t, uint32_t prime, int value_bytes, uintptr_t secrets,
+           uintptr_t matrix, int mask_mode, int seed_words, std::vector<uint32_t> rng,
+           uint64_t owner_base, uintptr_t shares, uintptr_t cnt, uintptr_t mask_out,
+           uintptr_t mask_cnt, uintptr_t seeds, uintptr_t err, uintptr_t stream) {
+          if (k > 8 || t > 16 || n > 64)
+            throw std::invalid_argument("share_pss: register kernel supports k<=8, t<=16, n<=64");
+          launch_share_pss(Pn, D, n, k, t, prime, value_bytes, P<const int32_t>(secrets),
+                           P<const uint32_t>(matrix), mask_mode, seed_words, rng_from(rng),
+                           owner_base, P<void>(shares), P<uint32_t>(cnt), P<uint32_t>(mask_out),
+                           P<uint32_t>(mask_cnt), P<uint32_t>(seeds), P<uint32_t>(err), S(stream));
+          check_launch("share_pss");
+        });
+  m.def("count", [](int M, int L, int value_bytes, uintptr_t vals, uintptr_t cnt, uintptr_t stream) {
+    launch_count(M, L, value_bytes, P<const void>(vals), P<uint32_t>(cnt), S(stream));
+    check_launch("count");
+  });
+  m.def("chacha_mask_sum", [](int Pn, int D, uint32_t mod, int seed_words, uintptr_t seeds,
+                              uintptr_t out, uintptr_t err, uintptr_t stream) {
+    launch_chacha_mask_sum(Pn, D, mod, seed_words, P<const uint32_t>(seeds), P<uint32_t>(out),
+                           P<uint32_t>(err), S(stream));
+    check_launch("chacha_mask_sum");
+  });
+  m.def("segscan", [](int M, int T, uintptr_t data, uintptr_t totals, uintptr_t stream) {
+    launch_segscan(M, T, P<uint32_t>(data), P<uint32_t>(totals), S(stream));
+    check_launch("segscan");
+  });
+  m.def("encode_encrypt", [](int M, int L, int value_bytes, uintptr_t vals, uintptr_t tile_off,
+                             uintptr_t keys, uintptr_t ct, uint64_t stride, uintptr_t stream) {
+    launch_encode_encrypt(M, L, value_bytes, P<const void>(vals), P<const uint32_t>(tile_off),
+                          P<const MsgKey>(keys), P<uint8_t>(ct), stride, S(stream));
+    check_launch("encode_encrypt");
+  });
+  m.def("mac_chunks", [](int M, int K, uintptr_t keys, uintptr_t ct, uint64_t stride,
+                         uintptr_t pt_len, uintptr_t partials, int decrypt, uintptr_t term_cnt,
+                         uintptr_t stream) {
+    launch_mac_chunks(M, K, P<const MsgKey>(keys), P<uint8_t>(ct), stride,
+                      P<const uint32_t>(pt_len), P<uint32_t>(partials), decrypt,
+                      P<uint32_t>(term_cnt), S(stream));
+    check_launch("mac_chunks");
+  });
+  m.def("mac_final", [](int M, int K, uintptr_t keys, uintptr_t ct, uint64_t stride,
+                        uintptr_t pt_len, uintptr_t partials, int verify, uintptr_t ok,
+                        uintptr_t err, uintptr_t stream) {
+    launch_mac_final(M, K, P<const MsgKey>(keys), P<uint8_t>(ct), stride,
+                     P<const uint32_t>(pt_len), P<const uint32_t>(partials), verify,
+                     P<uint32_t>(ok), P<uint32_t>(err), S(stream));
+    check_launch("mac_final");
+  });
+  m.def("decode", [](int M, int K, int L, uint32_t mod, int value_bytes, uintptr_t pt,
+                     uint64_t stride, uintptr_t pt_len, uintptr_t elem_start, uintptr_t vals,
+                     uintptr_t err, uintptr_t stream) {
+    launch_decode(M, K, L, mod, value_bytes, P<const uint8_t>(pt), stride,
+                  P<const uint32_t>(pt_len), P<const uint32_t>(elem_start), P<void>(vals),
+                  P<uint32_t>(err), S(stream));
+    check_launch("decode");
+  });
+  m.def("colsum", [](int G, int R, int L, uint32_t mod, int value_bytes, uintptr_t vals,
+                     uintptr_t out, uintptr_t stream) {
+    launch_colsum(G, R, L, mod, value_bytes, P<const void>(vals), P<uint32_t>(out), S(stream));
+    check_launch("colsum");
+  });
+  m.def("pss_reconstruct", [](int B, int k, int nI, int D, uint32_t prime, uintptr_t lag,
+                              uintptr_t ys, uintptr_t out, uintptr_t stream) {
+    launch_pss_reconstruct(B, k, nI, D, prime, P<const uint32_t>(lag), P<const uint32_t>(ys),
+                           P<uint32_t>(out), S(stream));
+    check_launch("pss_reconstruct");
+  });
+  m.def("sub_mod", [](int D, uint32_t mod, uintptr_t a, uintptr_t b, uintptr_t out,
+                      uintptr_t stream) {
+    launch_sub_mod(D, mod, P<const uint32_t>(a), P<const uint32_t>(b), P<uint32_t>(out), S(stream));
+    check_launch("sub_mod");
+  });
+}

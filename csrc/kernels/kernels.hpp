@@ -1,0 +1,124 @@
+// Host-side launch API of the SDA HIP kernels (gfx950).
+//
+// All buffers are raw device pointers owned by the caller (PyTorch tensors in the
+// Python engine); every launcher is asynchronous on the given stream and does no
+// allocation or synchronisation, so a whole aggregation round can be captured
+// into a hipGraph.
+//
+// Message model (shared by every kernel): a *message* is one sealed box
+// (libsodium crypto_box_seal, reference sodium.rs:36-43) over the zigzag-varint
+// encoding of a vector of L field values. Messages of one launch have a uniform
+// value count L and live in a ciphertext arena at `ct + j*stride` laid out as
+//   epk(32) | mac(16) | ct bytes (<= L*maxlen) | padding   (stride % 64 == 0).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace sdagpu {
+
+// Per-message stream state derived by the seal/open setup kernels.
+struct MsgKey {
+  uint32_t subkey[8];   // XSalsa20 subkey = HSalsa20(k, nonce[0:16])
+  uint32_t nonce[2];    // nonce[16:24]
+  uint32_t poly_r[4];   // keystream bytes 0..15
+  uint32_t poly_s[4];   // keystream bytes 16..31
+  uint32_t pad[2];
+};
+static_assert(sizeof(MsgKey) == 80, "MsgKey layout");
+
+constexpr int kTileValues = 4096;   // values per encode tile (256 threads x 16)
+constexpr int kChunkBytes = 16384;  // bytes per MAC / decrypt chunk (256 threads x 64)
+
+// Error bits (device error word)
+enum ErrBits : uint32_t {
+  kErrBadKey = 1u,          // X25519 produced the all-zero point
+  kErrMac = 2u,             // Poly1305 verification failed
+  kErrMalformed = 4u,       // varint stream does not hold exactly L values
+  kErrChaChaReject = 8u,    // rand-0.3 ChaCha mask hit a rejection (host fallback)
+  kErrRange = 16u,          // value outside the expected modulus
+};
+
+struct RngKeyArg {
+  uint32_t k[8];
+};
+
+// ---- keys.hip --------------------------------------------------------------
+// Seal setup: esk from the device CSPRNG (purpose ephemeral, owner
+// msg_owner_base + j), epk -> header, MsgKey for encryption.
+void launch_seal_setup(int M, RngKeyArg rng, uint64_t msg_owner_base, const uint32_t* key_idx,
+                       const uint32_t* pks, uint8_t* ct, uint64_t stride, MsgKey* keys,
+                       uint32_t* err, hipStream_t s);
+// Open setup: epk from header, X25519 with the recipient secret key.
+void launch_open_setup(int M, const uint32_t* key_idx, const uint32_t* sks, const uint32_t* pks,
+                       const uint8_t* ct, uint64_t stride, MsgKey* keys, uint32_t* err,
+                       hipStream_t s);
+// Standalone batched X25519 (tests / key generation): out[i] = X25519(sc[i], u[i]).
+void launch_x25519(int N, const uint32_t* scalars, const uint32_t* points, uint32_t* out,
+                   hipStream_t s);
+
+// ---- share.hip -------------------------------------------------------------
+enum MaskMode : int { kMaskNone = 0, kMaskFull = 1, kMaskChaCha = 2 };
+
+// Additive sharing (client/src/crypto/sharing/additive.rs:32-51 semantics, canonical
+// representatives) fused with masking and per-tile varint byte counts.
+//   secrets  [P][D] int32 ; shares [n][P][D] (u16 if value_bytes==2 else u32)
+//   cnt      [n][P][T] tile byte counts (T = ceil(D / kTileValues))
+//   mask_out [P][D] u32 (kMaskFull) and mask_cnt [P][T]
+//   seeds    [P][seed_words] u32 (kMaskChaCha, produced here from the CSPRNG)
+void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, const int32_t* secrets,
+                           int mask_mode, int seed_words, RngKeyArg rng, uint64_t owner_base,
+                           void* shares, uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt,
+                           uint32_t* seeds, uint32_t* err, hipStream_t s);
+
+// Packed Shamir: shares = M . [s_1..s_k, r_1..r_t] mod p per batch (M: n x (k+t)
+// host-computed from the tss FFT construction).
+void launch_share_pss(int P, int D, int n, int k, int t, uint32_t p, int value_bytes,
+                      const int32_t* secrets, const uint32_t* share_matrix, int mask_mode,
+                      int seed_words, RngKeyArg rng, uint64_t owner_base, void* shares,
+                      uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt, uint32_t* seeds,
+                      uint32_t* err, hipStream_t s);
+
+// Tile byte counts for arbitrary canonical value vectors [M][L].
+void launch_count(int M, int L, int value_bytes, const void* vals, uint32_t* cnt, hipStream_t s);
+
+// rand-0.3 ChaChaRng mask expansion summed over participants:
+//   out[e] = sum_p gen_range(0, m)_e(seed_p) mod m      (chacha.rs:56-77)
+void launch_chacha_mask_sum(int P, int D, uint32_t m, int seed_words, const uint32_t* seeds,
+                            uint32_t* out, uint32_t* err, hipStream_t s);
+
+// ---- seal.hip --------------------------------------------------------------
+// Segmented exclusive scan of rows [M][T] in place; totals[M] = row sums.
+void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, hipStream_t s);
+// Varint-encode + XSalsa20-encrypt tiles into the arena (ct bytes only).
+void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
+                           const uint32_t* tile_off, const MsgKey* keys, uint8_t* ct,
+                           uint64_t stride, hipStream_t s);
+// Poly1305 chunk partials (and, when decrypt!=0, in-place decryption plus
+// varint-terminator counts per chunk).
+void launch_mac_chunks(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,
+                       const uint32_t* pt_len, uint32_t* partials, int decrypt,
+                       uint32_t* term_cnt, hipStream_t s);
+// Combine partials -> tag; mode 0 = write the header mac, 1 = verify (ok[j]).
+void launch_mac_final(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,
+                      const uint32_t* pt_len, const uint32_t* partials, int verify,
+                      uint32_t* ok, uint32_t* err, hipStream_t s);
+
+// ---- open.hip --------------------------------------------------------------
+// Decode the plaintext varint stream of each message into canonical values.
+void launch_decode(int M, int K, int L, uint32_t m, int value_bytes, const uint8_t* pt,
+                   uint64_t stride, const uint32_t* pt_len, const uint32_t* elem_start,
+                   void* vals, uint32_t* err, hipStream_t s);
+// Column sums mod m: out[g][l] = sum_r vals[g][r][l] mod m.
+void launch_colsum(int G, int R, int L, uint32_t m, int value_bytes, const void* vals,
+                   uint32_t* out, hipStream_t s);
+// Packed Shamir reconstruction: out[b*k + s] = sum_i lag[s][i] * ys[i][b] mod p,
+// truncated to D (batched.rs:68-99 + tss reconstruct).
+void launch_pss_reconstruct(int B, int k, int nI, int D, uint32_t p, const uint32_t* lag,
+                            const uint32_t* ys, uint32_t* out, hipStream_t s);
+// out[e] = (a[e] - b[e]) mod m  (unmask, full.rs:54-67 / chacha.rs:79-93)
+void launch_sub_mod(int D, uint32_t m, const uint32_t* a, const uint32_t* b, uint32_t* out,
+                    hipStream_t s);
+
+}  // namespace sdagpu

@@ -1,0 +1,136 @@
+// Sealed-box key setup kernels: one lane per message runs the X25519 ladder(s),
+// the BLAKE2b-192 nonce and the HSalsa20 derivations of libsodium's
+// crypto_box_seal / crypto_box_seal_open (reference sodium.rs:43,78).
+//
+// These are latency-bound (a 255-step ladder per lane) but tiny in count
+// (one per message), so the engine runs them on a side stream concurrently with
+// the bandwidth-bound share/encode kernels.
+#include "device_crypto.hpp"
+#include "kernels.hpp"
+
+namespace sdagpu {
+namespace {
+
+SDA_DEV void derive_msg_key(MsgKey& out, const uint32_t (&shared)[8], const uint32_t (&epk)[8],
+                            const uint32_t (&pk)[8]) {
+  const uint32_t zero4[4] = {0, 0, 0, 0};
+  uint32_t k[8];
+  hsalsa20(k, shared, zero4);  // crypto_box_beforenm
+  uint32_t msg[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { msg[i] = epk[i]; msg[8 + i] = pk[i]; }
+  uint32_t nonce[6];
+  blake2b_192_64(nonce, msg);
+  const uint32_t n4[4] = {nonce[0], nonce[1], nonce[2], nonce[3]};
+  uint32_t sub[8];
+  hsalsa20(sub, k, n4);
+  uint32_t b0[16];
+  salsa20_block(b0, sub, nonce[4], nonce[5], 0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out.subkey[i] = sub[i];
+  out.nonce[0] = nonce[4];
+  out.nonce[1] = nonce[5];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { out.poly_r[i] = b0[i]; out.poly_s[i] = b0[4 + i]; }
+  out.pad[0] = out.pad[1] = 0;
+}
+
+__global__ void __launch_bounds__(64) k_seal_setup(int M, RngKeyArg rng, uint64_t owner_base,
+                                                   const uint32_t* __restrict__ key_idx,
+                                                   const uint32_t* __restrict__ pks, uint8_t* ct,
+                                                   uint64_t stride, MsgKey* keys, uint32_t* err) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= M) return;
+  RngKey rk;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rk.k[i] = rng.k[i];
+  uint32_t w[16];
+  rng_block(w, rk, stream_id(kPurposeEphemeral, owner_base + (uint64_t)j), 0);
+  uint32_t esk[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) esk[i] = w[i];
+  const uint32_t nine[8] = {9, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t epk[8];
+  x25519(epk, esk, nine);
+  uint32_t pk[8];
+  const uint32_t* pkp = pks + 8 * (size_t)key_idx[j];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pk[i] = pkp[i];
+  uint32_t shared[8];
+  x25519(shared, esk, pk);
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc |= shared[i];
+  if (acc == 0) atomicOr(err, kErrBadKey);
+  MsgKey mk;
+  derive_msg_key(mk, shared, epk, pk);
+  keys[j] = mk;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(ct + (size_t)j * stride);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) hdr[i] = epk[i];
+}
+
+__global__ void __launch_bounds__(64) k_open_setup(int M, const uint32_t* __restrict__ key_idx,
+                                                   const uint32_t* __restrict__ sks,
+                                                   const uint32_t* __restrict__ pks,
+                                                   const uint8_t* ct, uint64_t stride,
+                                                   MsgKey* keys, uint32_t* err) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= M) return;
+  const uint32_t* hdr = reinterpret_cast<const uint32_t*>(ct + (size_t)j * stride);
+  uint32_t epk[8], sk[8], pk[8];
+  const size_t kix = key_idx[j];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    epk[i] = hdr[i];
+    sk[i] = sks[8 * kix + i];
+    pk[i] = pks[8 * kix + i];
+  }
+  uint32_t shared[8];
+  x25519(shared, sk, epk);
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc |= shared[i];
+  if (acc == 0) atomicOr(err, kErrBadKey);
+  MsgKey mk;
+  derive_msg_key(mk, shared, epk, pk);
+  keys[j] = mk;
+}
+
+__global__ void __launch_bounds__(64) k_x25519(int N, const uint32_t* __restrict__ sc,
+                                               const uint32_t* __restrict__ pt, uint32_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  uint32_t a[8], b[8], o[8];
+#pragma unroll
+  for (int w = 0; w < 8; ++w) { a[w] = sc[8 * (size_t)i + w]; b[w] = pt[8 * (size_t)i + w]; }
+  x25519(o, a, b);
+#pragma unroll
+  for (int w = 0; w < 8; ++w) out[8 * (size_t)i + w] = o[w];
+}
+
+}  // namespace
+
+void launch_seal_setup(int M, RngKeyArg rng, uint64_t owner_base, const uint32_t* key_idx,
+                       const uint32_t* pks, uint8_t* ct, uint64_t stride, MsgKey* keys,
+                       uint32_t* err, hipStream_t s) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(k_seal_setup, dim3((M + 63) / 64), dim3(64), 0, s, M, rng, owner_base,
+                     key_idx, pks, ct, stride, keys, err);
+}
+
+void launch_open_setup(int M, const uint32_t* key_idx, const uint32_t* sks, const uint32_t* pks,
+                       const uint8_t* ct, uint64_t stride, MsgKey* keys, uint32_t* err,
+                       hipStream_t s) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(k_open_setup, dim3((M + 63) / 64), dim3(64), 0, s, M, key_idx, sks, pks, ct,
+                     stride, keys, err);
+}
+
+void launch_x25519(int N, const uint32_t* scalars, const uint32_t* points, uint32_t* out,
+                   hipStream_t s) {
+  if (N <= 0) return;
+  hipLaunchKernelGGL(k_x25519, dim3((N + 63) / 64), dim3(64), 0, s, N, scalars, points, out);
+}
+
+}  // namespace sdagpu

@@ -1,0 +1,210 @@
+// Clerk / recipient kernels after decryption: parallel varint decode, the
+// per-clerk modular combine, packed-Shamir (Lagrange) reconstruction, unmask.
+//
+// Reference: sodium.rs:83-89 (decode until exhausted), sharing/combiner.rs:15-29
+// (element-wise sum mod m), sharing/batched.rs:68-99 + tss reconstruct
+// (reconstruct per batch, truncate to the dimension), masking/full.rs:54-67.
+//
+// Parallel decode: every byte with MSB = 0 terminates a varint, so a chunk's
+// terminator count gives element ranks by an exclusive scan across chunks
+// (launch_segscan over the per-chunk counts from k_mac_chunks<1>); inside a chunk
+// the lanes rank their terminators with a block scan and each lane decodes the
+// varints ending in its 64 bytes, reading at most 9 bytes back (a 16-byte LDS
+// prefix of the previous chunk covers varints straddling the boundary).
+#include "block_utils.hpp"
+#include "device_crypto.hpp"
+#include "kernels.hpp"
+#include "modarith.hpp"
+
+namespace sdagpu {
+namespace {
+
+template <typename VT>
+__global__ void __launch_bounds__(kBlock)
+    k_decode(int L, ModParams mp, const uint8_t* __restrict__ pt, uint64_t stride,
+             const uint32_t* __restrict__ pt_len, const uint32_t* __restrict__ elem_start,
+             VT* __restrict__ vals, uint32_t* err) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kChunkBytes + 16];
+  __shared__ uint32_t scratch[kWaves];
+  const int k = blockIdx.x, j = blockIdx.y, K = gridDim.x;
+  const int tid = threadIdx.x;
+  const uint32_t N = pt_len[j];
+  const int64_t kC = (int64_t)k * kChunkBytes;
+  const int64_t start = kC >= 32 ? kC - 32 : 0;
+  const int64_t end = min((int64_t)N, kC + kChunkBytes - 32);
+  if (start >= end) return;
+  const uint8_t* gmsg = pt + (size_t)j * stride + 48;
+  // LDS image: index 16 + (pos - (kC - 32)); prefix [0,16) = 16 bytes before the chunk
+  const int64_t base = kC - 48;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int off = 64 * tid + 16 * q;
+    const int64_t pos = kC - 32 + off;
+    if (pos >= 0 && pos < end)
+      *reinterpret_cast<uint4*>(buf + 16 + off) = *reinterpret_cast<const uint4*>(gmsg + pos);
+  }
+  if (tid == 0 && base >= 0)
+    *reinterpret_cast<uint4*>(buf) = *reinterpret_cast<const uint4*>(gmsg + base);
+  __syncthreads();
+  // rank terminators
+  uint32_t cnt = 0;
+  for (int b = 0; b < 64; ++b) {
+    const int64_t pos = kC - 32 + 64 * tid + b;
+    if (pos >= start && pos < end && !(buf[16 + 64 * tid + b] & 0x80)) ++cnt;
+  }
+  uint32_t tot;
+  uint32_t rank = elem_start[(size_t)j * K + k] + block_excl_scan(cnt, scratch, &tot);
+  VT* out = vals + (size_t)j * L;
+  bool bad = false;
+  for (int b = 0; b < 64; ++b) {
+    const int64_t pos = kC - 32 + 64 * tid + b;
+    if (pos < start || pos >= end) continue;
+    const uint32_t byte = buf[16 + 64 * tid + b];
+    if (byte & 0x80) {
+      if (pos == (int64_t)N - 1) bad = true;  // dangling continuation byte
+      continue;
+    }
+    // find the first byte of this varint
+    int64_t s = pos;
+    int steps = 0;
+    while (s > 0 && steps < 10 && (buf[16 + (s - 1) - (kC - 32)] & 0x80)) {
+      --s;
+      ++steps;
+    }
+    if (steps >= 10) { bad = true; ++rank; continue; }
+    uint64_t z = 0;
+    for (int64_t u = s; u <= pos; ++u) z |= (uint64_t)(buf[16 + u - (kC - 32)] & 0x7f) << (7 * (u - s));
+    // unzigzag, canonicalise
+    uint32_t val;
+    if (!(z & 1)) {
+      uint64_t mag = z >> 1;
+      if (mp.m == 0) {
+        if (mag > 0xffffffffULL) bad = true;
+        val = (uint32_t)mag;
+      } else {
+        val = mag < mp.m ? (uint32_t)mag : mod64(mag, mp);
+      }
+    } else {
+      uint64_t mag = (z >> 1) + 1;  // value = -mag
+      if (mp.m == 0) { bad = true; val = 0; }
+      else {
+        uint32_t r = mod64(mag, mp);
+        val = r == 0 ? 0u : mp.m - r;
+      }
+    }
+    if (rank < (uint32_t)L) out[rank] = (VT)val;
+    else bad = true;
+    ++rank;
+  }
+  if (bad) atomicOr(err, kErrMalformed);
+}
+
+template <typename VT, typename ACC>
+__global__ void __launch_bounds__(kBlock)
+    k_colsum(int R, int L, ModParams mp, const VT* __restrict__ vals, uint32_t* __restrict__ out) {
+  const int g = blockIdx.y;
+  const int l0 = (blockIdx.x * kBlock + threadIdx.x) * 8;
+  if (l0 >= L) return;
+  const VT* src = vals + (size_t)g * R * L;
+  ACC acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool vec = (L % 8) == 0;
+  if (vec) {
+    for (int r = 0; r < R; ++r) {
+      const VT* row = src + (size_t)r * L + l0;
+      if constexpr (sizeof(VT) == 2) {
+        uint4 q = *reinterpret_cast<const uint4*>(row);
+        acc[0] += q.x & 0xffff; acc[1] += q.x >> 16; acc[2] += q.y & 0xffff; acc[3] += q.y >> 16;
+        acc[4] += q.z & 0xffff; acc[5] += q.z >> 16; acc[6] += q.w & 0xffff; acc[7] += q.w >> 16;
+      } else {
+        uint4 a = reinterpret_cast<const uint4*>(row)[0];
+        uint4 b = reinterpret_cast<const uint4*>(row)[1];
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+      }
+    }
+  } else {
+    for (int r = 0; r < R; ++r) {
+      const VT* row = src + (size_t)r * L;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (l0 + i < L) acc[i] += row[l0 + i];
+    }
+  }
+  uint32_t* o = out + (size_t)g * L;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (l0 + i < L) o[l0 + i] = mod64((uint64_t)acc[i], mp);
+}
+
+__global__ void __launch_bounds__(kBlock)
+    k_pss_reconstruct(int B, int k, int nI, int D, ModParams mp, const uint32_t* __restrict__ lag,
+                      const uint32_t* __restrict__ ys, uint32_t* __restrict__ out) {
+  extern __shared__ uint32_t sL[];
+  for (int i = threadIdx.x; i < k * nI; i += kBlock) sL[i] = lag[i];
+  __syncthreads();
+  const int b = blockIdx.x * kBlock + threadIdx.x;
+  if (b >= B) return;
+  for (int s = 0; s < k; ++s) {
+    const int e = b * k + s;
+    if (e >= D) break;
+    uint32_t acc = 0;
+    for (int i = 0; i < nI; ++i)
+      acc = add_mod(acc, mod64((uint64_t)sL[s * nI + i] * ys[(size_t)i * B + b], mp), mp.m);
+    out[e] = acc;
+  }
+}
+
+__global__ void k_sub_mod(int D, uint32_t m, const uint32_t* __restrict__ a,
+                          const uint32_t* __restrict__ b, uint32_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < D) out[i] = sub_mod(a[i], b[i], m);
+}
+
+}  // namespace
+
+void launch_decode(int M, int K, int L, uint32_t m, int value_bytes, const uint8_t* pt,
+                   uint64_t stride, const uint32_t* pt_len, const uint32_t* elem_start,
+                   void* vals, uint32_t* err, hipStream_t s) {
+  if (M <= 0 || K <= 0) return;
+  ModParams mp = make_mod_params(m);
+  dim3 grid(K, M);
+  if (value_bytes == 2)
+    hipLaunchKernelGGL(k_decode<uint16_t>, grid, dim3(kBlock), 0, s, L, mp, pt, stride, pt_len,
+                       elem_start, (uint16_t*)vals, err);
+  else
+    hipLaunchKernelGGL(k_decode<uint32_t>, grid, dim3(kBlock), 0, s, L, mp, pt, stride, pt_len,
+                       elem_start, (uint32_t*)vals, err);
+}
+
+void launch_colsum(int G, int R, int L, uint32_t m, int value_bytes, const void* vals,
+                   uint32_t* out, hipStream_t s) {
+  if (G <= 0 || L <= 0) return;
+  ModParams mp = make_mod_params(m);
+  const int threads = (L + 7) / 8;
+  dim3 grid((threads + kBlock - 1) / kBlock, G);
+  if (value_bytes == 2 && (uint64_t)R * 65535ull < 0xffffffffull)
+    hipLaunchKernelGGL((k_colsum<uint16_t, uint32_t>), grid, dim3(kBlock), 0, s, R, L, mp,
+                       (const uint16_t*)vals, out);
+  else if (value_bytes == 2)
+    hipLaunchKernelGGL((k_colsum<uint16_t, uint64_t>), grid, dim3(kBlock), 0, s, R, L, mp,
+                       (const uint16_t*)vals, out);
+  else
+    hipLaunchKernelGGL((k_colsum<uint32_t, uint64_t>), grid, dim3(kBlock), 0, s, R, L, mp,
+                       (const uint32_t*)vals, out);
+}
+
+void launch_pss_reconstruct(int B, int k, int nI, int D, uint32_t p, const uint32_t* lag,
+                            const uint32_t* ys, uint32_t* out, hipStream_t s) {
+  if (B <= 0) return;
+  ModParams mp = make_mod_params(p);
+  hipLaunchKernelGGL(k_pss_reconstruct, dim3((B + kBlock - 1) / kBlock), dim3(kBlock),
+                     (size_t)k * nI * sizeof(uint32_t), s, B, k, nI, D, mp, lag, ys, out);
+}
+
+void launch_sub_mod(int D, uint32_t m, const uint32_t* a, const uint32_t* b, uint32_t* out,
+                    hipStream_t s) {
+  if (D <= 0) return;
+  hipLaunchKernelGGL(k_sub_mod, dim3((D + 255) / 256), dim3(256), 0, s, D, m, a, b, out);
+}
+
+}  // namespace sdagpu

@@ -1,0 +1,322 @@
+// Sealed-box bulk kernels: varint encode + XSalsa20 encrypt, and the parallel
+// Poly1305 MAC (optionally fused with in-place decryption + varint terminator
+// counting for the clerk/recipient side).
+//
+// Reference: sodium.rs:36-43 (encode each share with zigzag LEB128, then
+// sealedbox::seal) and sodium.rs:78-89 (open, then decode until exhausted).
+//
+// Parallel Poly1305: a message is cut into 16 KiB chunks aligned to the keystream
+// (chunk k covers keystream bytes [kC, (k+1)C), i.e. message bytes
+// [kC-32, (k+1)C-32)). Inside a chunk each lane runs Horner over 4 consecutive
+// 16-byte blocks, end-aligned to the chunk's last block so that absent leading
+// blocks contribute exactly zero, and lanes are merged by a log-depth tree with
+// r^(4*2^l). A per-message pass chains the chunk partials with r^(C/16).
+#include "block_utils.hpp"
+#include "device_crypto.hpp"
+#include "kernels.hpp"
+
+namespace sdagpu {
+namespace {
+
+constexpr int kLdsEncodeBytes = kTileValues * 5 + 128;
+
+template <typename VT>
+__global__ void __launch_bounds__(kBlock)
+    k_encode_encrypt(int L, const VT* __restrict__ vals, const uint32_t* __restrict__ tile_off,
+                     const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct, uint64_t stride) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEncodeBytes];
+  __shared__ uint32_t scratch[kWaves];
+  const int t = blockIdx.x, j = blockIdx.y, T = gridDim.x;
+  const int tid = threadIdx.x;
+  const int e0 = t * kTileValues + tid * 16;
+  const VT* src = vals + (size_t)j * L;
+  uint32_t v[16];
+  uint32_t my_bytes = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    v[i] = (e0 + i < L) ? (uint32_t)src[e0 + i] : 0u;
+    if (e0 + i < L) {
+      uint64_t z = (uint64_t)v[i] << 1;
+      my_bytes += 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
+    }
+  }
+  uint32_t tile_bytes;
+  const uint32_t excl = block_excl_scan(my_bytes, scratch, &tile_bytes);
+  const uint32_t a = tile_off[(size_t)j * T + t];
+  const uint32_t b0 = (32u + a) >> 6;
+  const uint32_t base = 32u + a - 64u * b0;  // LDS index of message byte `a`
+  uint32_t pos = base + excl;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (e0 + i < L) {
+      uint64_t z = (uint64_t)v[i] << 1;
+      for (;;) {
+        uint8_t byte = (uint8_t)(z & 0x7f);
+        z >>= 7;
+        if (z) { lds[pos++] = byte | 0x80; } else { lds[pos++] = byte; break; }
+      }
+    }
+  }
+  __syncthreads();
+  const MsgKey key = keys[j];
+  const uint32_t nblk = (base + tile_bytes + 63) >> 6;
+  for (uint32_t blk = tid; blk < nblk; blk += kBlock) {
+    uint32_t w[16];
+    salsa20_block(w, key.subkey, key.nonce[0], key.nonce[1], (uint64_t)(b0 + blk));
+    uint4* q = reinterpret_cast<uint4*>(lds + 64 * blk);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      uint4 d = q[u];
+      d.x ^= w[4 * u]; d.y ^= w[4 * u + 1]; d.z ^= w[4 * u + 2]; d.w ^= w[4 * u + 3];
+      q[u] = d;
+    }
+  }
+  __syncthreads();
+  uint8_t* gmsg = ct + (size_t)j * stride + 48;
+  const uint32_t lo = a & ~15u, hi = (a + tile_bytes + 15u) & ~15u, end = a + tile_bytes;
+  for (uint32_t c = lo + 16u * tid; c < hi; c += 16u * kBlock) {
+    if (c >= a && c + 16u <= end) {
+      *reinterpret_cast<uint4*>(gmsg + c) = *reinterpret_cast<const uint4*>(lds + (c - a + base));
+    } else {
+      for (uint32_t q = 0; q < 16; ++q) {
+        uint32_t p = c + q;
+        if (p >= a && p < end) gmsg[p] = lds[p - a + base];
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_segscan(int T, uint32_t* __restrict__ data,
+                                                    uint32_t* __restrict__ totals) {
+  __shared__ uint32_t scratch[kWaves];
+  uint32_t* row = data + (size_t)blockIdx.x * T;
+  uint32_t carry = 0;
+  for (int b = 0; b < T; b += kBlock) {
+    const int i = b + threadIdx.x;
+    uint32_t v = i < T ? row[i] : 0u;
+    uint32_t tot;
+    uint32_t ex = block_excl_scan(v, scratch, &tot);
+    if (i < T) row[i] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0 && totals) totals[blockIdx.x] = carry;
+}
+
+// Read 16 plaintext/ciphertext bytes as a Poly1305 block (block index i of a
+// message of N bytes), from the chunk LDS image whose index 0 is keystream byte kC.
+SDA_DEV P130 load_block(const uint8_t* lds, int64_t i, int64_t kC, uint32_t N) {
+  const int64_t off = 32 + 16 * i - kC;
+  const uint4 q = *reinterpret_cast<const uint4*>(lds + off);
+  uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  uint32_t hibit = 1u << 24;
+  const int64_t rem = (int64_t)N - 16 * i;
+  if (rem < 16) {
+    // partial final block: keep `rem` bytes, append 0x01, zero the rest
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const int wi = b >> 2, sh = (b & 3) * 8;
+      uint32_t byte = (w[wi] >> sh) & 0xff;
+      uint32_t nb = b < rem ? byte : (b == rem ? 1u : 0u);
+      w[wi] = (w[wi] & ~(0xffu << sh)) | (nb << sh);
+    }
+    hibit = 0;
+  }
+  return p130_block(w[0], w[1], w[2], w[3], hibit);
+}
+
+template <int DECRYPT>
+__global__ void __launch_bounds__(kBlock)
+    k_mac_chunks(const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct, uint64_t stride,
+                 const uint32_t* __restrict__ pt_len, uint32_t* __restrict__ partials,
+                 uint32_t* __restrict__ term_cnt) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kChunkBytes];
+  __shared__ uint32_t tree[5][kBlock];
+  __shared__ uint32_t scratch[kWaves];
+  const int k = blockIdx.x, j = blockIdx.y, K = gridDim.x;
+  const int tid = threadIdx.x;
+  const uint32_t N = pt_len[j];
+  const int64_t kC = (int64_t)k * kChunkBytes;
+  const int64_t start = kC >= 32 ? kC - 32 : 0;
+  const int64_t end = min((int64_t)N, kC + kChunkBytes - 32);
+  uint32_t* part = partials + ((size_t)j * K + k) * 8;
+  if (start >= end) {  // chunk beyond the message (or empty message)
+    if (tid < 5) part[tid] = 0;
+    if (DECRYPT && tid == 0) term_cnt[(size_t)j * K + k] = 0;
+    return;
+  }
+  uint8_t* gmsg = ct + (size_t)j * stride + 48;
+  // load the chunk (16-byte pieces overlapping [start, end))
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int off = 64 * tid + 16 * q;
+    const int64_t pos = kC - 32 + off;
+    if (pos >= start - 15 && pos >= 0 && pos < end)
+      *reinterpret_cast<uint4*>(buf + off) = *reinterpret_cast<const uint4*>(gmsg + pos);
+  }
+  __syncthreads();
+
+  // ---- Poly1305 partial over blocks [fb, eb)
+  const MsgKey key = keys[j];
+  const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
+  const P130 r = p130_r_from_key(rk);
+  const int64_t fb = start / 16;
+  const int64_t eb = (end + 15) / 16;
+  P130 h = p130_zero();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t i = eb - 4 * (int64_t)(kBlock - tid) + q;
+    P130 c = p130_zero();
+    if (i >= fb) c = load_block(buf, i, kC, N);
+    h = p130_mul(p130_add(h, c), r);
+  }
+  P130 R = p130_mul(r, r);
+  R = p130_mul(R, R);  // r^4
+#pragma unroll
+  for (int l = 0; l < 8; ++l) {
+    const int s = 1 << l;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 5; ++u) tree[u][tid] = h.v[u];
+    __syncthreads();
+    if ((tid & (2 * s - 1)) == 2 * s - 1) {
+      P130 left;
+#pragma unroll
+      for (int u = 0; u < 5; ++u) left.v[u] = tree[u][tid - s];
+      h = p130_carry(p130_add(p130_mul(left, R), h));
+    }
+    R = p130_mul(R, R);
+  }
+  if (tid == kBlock - 1) {
+#pragma unroll
+    for (int u = 0; u < 5; ++u) part[u] = h.v[u];
+  }
+
+  if constexpr (DECRYPT) {
+    // keystream block b covers message bytes [64b-32, 64b+32)
+    const int64_t b = kC / 64 + tid;
+    const int64_t lo = 64 * b - 32;
+    if (lo < end && lo + 64 > start) {
+      uint32_t w[16];
+      salsa20_block(w, key.subkey, key.nonce[0], key.nonce[1], (uint64_t)b);
+      uint4* q = reinterpret_cast<uint4*>(buf + 64 * tid);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        uint4 d = q[u];
+        d.x ^= w[4 * u]; d.y ^= w[4 * u + 1]; d.z ^= w[4 * u + 2]; d.w ^= w[4 * u + 3];
+        q[u] = d;
+      }
+    }
+    // terminators (MSB clear) among this lane's valid bytes
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int off = 64 * tid + 16 * q;
+      const uint4 d = *reinterpret_cast<const uint4*>(buf + off);
+      const uint32_t ws[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+      for (int bb = 0; bb < 16; ++bb) {
+        const int64_t pos = kC - 32 + off + bb;
+        const uint32_t byte = (ws[bb >> 2] >> ((bb & 3) * 8)) & 0xff;
+        cnt += (pos >= start && pos < end && !(byte & 0x80)) ? 1u : 0u;
+      }
+    }
+    const uint32_t tot = block_sum(cnt, scratch);
+    if (tid == 0) term_cnt[(size_t)j * K + k] = tot;
+    // store plaintext in place (bytes past `end` land in the slot padding)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int off = 64 * tid + 16 * q;
+      const int64_t pos = kC - 32 + off;
+      if (pos >= start - 15 && pos >= 0 && pos < end)
+        *reinterpret_cast<uint4*>(gmsg + pos) = *reinterpret_cast<const uint4*>(buf + off);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64)
+    k_mac_final(int M, int K, const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct,
+                uint64_t stride, const uint32_t* __restrict__ pt_len,
+                const uint32_t* __restrict__ partials, int verify, uint32_t* __restrict__ ok,
+                uint32_t* err) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= M) return;
+  const uint32_t N = pt_len[j];
+  const MsgKey key = keys[j];
+  const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
+  const P130 r = p130_r_from_key(rk);
+  const int Kc = (int)(((int64_t)N + 32 + kChunkBytes - 1) / kChunkBytes);
+  const P130 rC = p130_pow(r, kChunkBytes / 16);
+  P130 H = p130_zero();
+  int64_t prev = 0;
+  for (int k = 0; k < Kc && k < K; ++k) {
+    const int64_t e = (k < Kc - 1) ? ((int64_t)(k + 1) * kChunkBytes - 32) / 16 : ((int64_t)N + 15) / 16;
+    const uint32_t* pp = partials + ((size_t)j * K + k) * 8;
+    P130 hk = P130{{pp[0], pp[1], pp[2], pp[3], pp[4]}};
+    if (k == 0) {
+      H = hk;
+    } else {
+      const int64_t d = e - prev;
+      const P130 Rd = (d == kChunkBytes / 16) ? rC : p130_pow(r, (uint32_t)d);
+      H = p130_carry(p130_add(p130_mul(H, Rd), hk));
+    }
+    prev = e;
+  }
+  H = p130_mul(H, r);
+  const uint32_t s4[4] = {key.poly_s[0], key.poly_s[1], key.poly_s[2], key.poly_s[3]};
+  uint32_t tag[4];
+  p130_finish(tag, H, s4);
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(ct + (size_t)j * stride + 32);
+  if (!verify) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) hdr[i] = tag[i];
+  } else {
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) diff |= hdr[i] ^ tag[i];
+    if (ok) ok[j] = diff == 0 ? 1u : 0u;
+    if (diff) atomicOr(err, kErrMac);
+  }
+}
+
+}  // namespace
+
+void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, hipStream_t s) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(k_segscan, dim3(M), dim3(kBlock), 0, s, T, data, totals);
+}
+
+void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
+                           const uint32_t* tile_off, const MsgKey* keys, uint8_t* ct,
+                           uint64_t stride, hipStream_t s) {
+  if (M <= 0 || L <= 0) return;
+  dim3 grid((L + kTileValues - 1) / kTileValues, M);
+  if (value_bytes == 2)
+    hipLaunchKernelGGL(k_encode_encrypt<uint16_t>, grid, dim3(kBlock), 0, s, L,
+                       (const uint16_t*)vals, tile_off, keys, ct, stride);
+  else
+    hipLaunchKernelGGL(k_encode_encrypt<uint32_t>, grid, dim3(kBlock), 0, s, L,
+                       (const uint32_t*)vals, tile_off, keys, ct, stride);
+}
+
+void launch_mac_chunks(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,
+                       const uint32_t* pt_len, uint32_t* partials, int decrypt,
+                       uint32_t* term_cnt, hipStream_t s) {
+  if (M <= 0 || K <= 0) return;
+  dim3 grid(K, M);
+  if (decrypt)
+    hipLaunchKernelGGL(k_mac_chunks<1>, grid, dim3(kBlock), 0, s, keys, ct, stride, pt_len,
+                       partials, term_cnt);
+  else
+    hipLaunchKernelGGL(k_mac_chunks<0>, grid, dim3(kBlock), 0, s, keys, ct, stride, pt_len,
+                       partials, term_cnt);
+}
+
+void launch_mac_final(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,
+                      const uint32_t* pt_len, const uint32_t* partials, int verify,
+                      uint32_t* ok, uint32_t* err, hipStream_t s) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(k_mac_final, dim3((M + 63) / 64), dim3(64), 0, s, M, K, keys, ct, stride,
+                     pt_len, partials, verify, ok, err);
+}
+
+}  // namespace sdagpu

@@ -1,0 +1,439 @@
+// Participant-side kernels: masking + secret sharing + varint byte counting.
+//
+// Reference semantics:
+//  * additive sharing  client/src/crypto/sharing/additive.rs:32-51 (n-1 uniform
+//    shares, last = secret - sum), batched per clerk (batched.rs:19-52)
+//  * packed Shamir     client/src/crypto/sharing/packed_shamir.rs:40-43 -> tss
+//    share(); here as the equivalent n x (k+t) matrix product
+//  * masks             masking/full.rs:22-34 (uniform mask), masking/chacha.rs:22-53
+//    (rand-0.3 ChaChaRng expansion of a per-participant seed)
+//
+// Randomness: counter-mode ChaCha20 keyed per round from OS entropy, one stream
+// per (purpose, participant); every draw is exact-uniform (rejection with a
+// deterministic retry stream), so outputs are a pure function of (key, indices).
+// The share kernel writes shares clerk-major ([n][P][B]) so each clerk's block
+// is contiguous -- the "transpose" of the snapshot step (server/src/stores.rs:86-101)
+// is free.
+#include "block_utils.hpp"
+#include "device_crypto.hpp"
+#include "kernels.hpp"
+#include "modarith.hpp"
+
+namespace sdagpu {
+namespace {
+
+SDA_DEV RngKey to_key(const RngKeyArg& a) {
+  RngKey k;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) k.k[i] = a.k[i];
+  return k;
+}
+
+// zigzag-varint length of a canonical (non-negative, < 2^32) value
+SDA_DEV uint32_t vlen(uint32_t v) {
+  uint64_t z = (uint64_t)v << 1;
+  return 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
+}
+
+template <typename VT>
+SDA_DEV void store16(VT* dst, const uint32_t (&v)[16], int valid, bool vec_ok) {
+  if (vec_ok && valid == 16) {
+    if constexpr (sizeof(VT) == 2) {
+      uint4 a, b;
+      a.x = v[0] | (v[1] << 16); a.y = v[2] | (v[3] << 16);
+      a.z = v[4] | (v[5] << 16); a.w = v[6] | (v[7] << 16);
+      b.x = v[8] | (v[9] << 16); b.y = v[10] | (v[11] << 16);
+      b.z = v[12] | (v[13] << 16); b.w = v[14] | (v[15] << 16);
+      reinterpret_cast<uint4*>(dst)[0] = a;
+      reinterpret_cast<uint4*>(dst)[1] = b;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        reinterpret_cast<uint4*>(dst)[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < valid) dst[i] = (VT)v[i];
+  }
+}
+
+SDA_DEV void load16_secrets(uint32_t (&x)[16], const int32_t* src, int valid, bool vec_ok,
+                            const ModParams& mp) {
+  int32_t s[16];
+  if (vec_ok && valid == 16) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int4 a = reinterpret_cast<const int4*>(src)[q];
+      s[4 * q] = a.x; s[4 * q + 1] = a.y; s[4 * q + 2] = a.z; s[4 * q + 3] = a.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = i < valid ? src[i] : 0;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = canon_i32(s[i], mp);
+}
+
+// rand-0.3 ChaChaRng block `ctr` (128-bit counter, here < 2^64) for a seed.
+SDA_DEV void chacharng_block(uint32_t (&w)[16], const uint32_t (&key)[8], uint64_t ctr) {
+  uint32_t in[16] = {kSigma0, kSigma1, kSigma2, kSigma3, key[0], key[1], key[2], key[3],
+                     key[4],  key[5],  key[6],  key[7],  (uint32_t)ctr, (uint32_t)(ctr >> 32), 0, 0};
+  chacha_block<20>(w, in);
+}
+
+// ChaCha mask for 16 consecutive elements starting at e0 (e0 % 8 == 0).
+SDA_DEV void chacha_mask16(uint32_t (&mk)[16], const uint32_t (&key)[8], uint64_t e0,
+                           const ModParams& mp, uint32_t* err) {
+  uint32_t w[16];
+  bool rej = false;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    chacharng_block(w, key, e0 / 8 + half);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      uint64_t v = ((uint64_t)w[2 * i] << 32) | w[2 * i + 1];
+      rej |= v >= mp.zone64;
+      mk[8 * half + i] = mod64(v, mp);
+    }
+  }
+  if (rej) atomicOr(err, kErrChaChaReject);
+}
+
+SDA_DEV void load_seed_key(uint32_t (&key)[8], const uint32_t* seeds, int p, int seed_words) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) key[i] = i < seed_words ? seeds[(size_t)p * seed_words + i] : 0u;
+}
+
+SDA_DEV uint32_t draw(uint32_t w, const RngKey& rk, uint64_t retry_purpose, uint64_t owner,
+                      uint64_t idx, const ModParams& mp) {
+  if ((uint64_t)w < mp.zone32) return mod32(w, mp);
+  return uniform_fixup(rk, retry_purpose, owner, idx, mp.m, (uint32_t)mp.zone32);
+}
+
+__global__ void k_chacha_seeds(int P, int seed_words, RngKeyArg rng, uint64_t owner_base,
+                               uint32_t* seeds) {
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  RngKey rk = to_key(rng);
+  uint32_t w[16];
+  rng_block(w, rk, stream_id(kPurposeChaChaSeed, owner_base + p), 0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (i < seed_words) seeds[(size_t)p * seed_words + i] = w[i];
+}
+
+// ------------------------------------------------------------- additive ----
+template <typename VT, int MASK>
+__global__ void __launch_bounds__(kBlock)
+    k_share_additive(int P, int D, int n, ModParams mp, const int32_t* __restrict__ secrets,
+                     RngKeyArg rng, uint64_t owner_base, VT* __restrict__ shares,
+                     uint32_t* __restrict__ cnt, uint32_t* __restrict__ mask_out,
+                     uint32_t* __restrict__ mask_cnt, const uint32_t* __restrict__ seeds,
+                     int seed_words, uint32_t* err) {
+  __shared__ uint32_t scratch[kWaves];
+  const int t = blockIdx.x, p = blockIdx.y, T = gridDim.x;
+  const int tid = threadIdx.x;
+  const int e0 = t * kTileValues + tid * 16;
+  const int valid = max(0, min(16, D - e0));
+  const uint64_t owner = owner_base + (uint64_t)p;
+  const uint64_t gthread = (uint64_t)t * kBlock + tid;
+  const RngKey rk = to_key(rng);
+  const uint32_t m = mp.m;
+  const bool vec_ok = (D % 16) == 0;
+
+  uint32_t x[16];
+  load16_secrets(x, secrets + (size_t)p * D + e0, valid, vec_ok, mp);
+
+  if constexpr (MASK == kMaskFull) {
+    uint32_t w[16], mk[16];
+    rng_block(w, rk, stream_id(kPurposeMaskFull, owner), gthread);
+    uint32_t bytes = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      mk[i] = draw(w[i], rk, kPurposeMaskRetry, owner, (uint64_t)(e0 + i), mp);
+      x[i] = add_mod(x[i], mk[i], m);
+      bytes += i < valid ? vlen(mk[i]) : 0u;
+    }
+    store16<uint32_t>(mask_out + (size_t)p * D + e0, mk, valid, vec_ok);
+    uint32_t tot = block_sum(bytes, scratch);
+    if (tid == 0) mask_cnt[(size_t)p * T + t] = tot;
+  } else if constexpr (MASK == kMaskChaCha) {
+    uint32_t key[8], mk[16];
+    load_seed_key(key, seeds, p, seed_words);
+    chacha_mask16(mk, key, (uint64_t)e0, mp, err);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = add_mod(x[i], mk[i], m);
+  }
+
+  uint32_t sum[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sum[i] = 0;
+  const int w_draws = n - 1;
+  for (int c = 0; c < w_draws; ++c) {
+    uint32_t w[16], r[16];
+    rng_block(w, rk, stream_id(kPurposeShares, owner), gthread * (uint64_t)w_draws + c);
+    uint32_t bytes = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      r[i] = draw(w[i], rk, kPurposeSharesRetry, owner,
+                  (uint64_t)(e0 + i) * (uint64_t)w_draws + c, mp);
+      sum[i] = add_mod(sum[i], r[i], m);
+      bytes += i < valid ? vlen(r[i]) : 0u;
+    }
+    store16<VT>(shares + ((size_t)c * P + p) * D + e0, r, valid, vec_ok);
+    uint32_t tot = block_sum(bytes, scratch);
+    if (tid == 0) cnt[((size_t)c * P + p) * T + t] = tot;
+  }
+  {
+    uint32_t r[16];
+    uint32_t bytes = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      r[i] = sub_mod(x[i], sum[i], m);
+      bytes += i < valid ? vlen(r[i]) : 0u;
+    }
+    const int c = n - 1;
+    store16<VT>(shares + ((size_t)c * P + p) * D + e0, r, valid, vec_ok);
+    uint32_t tot = block_sum(bytes, scratch);
+    if (tid == 0) cnt[((size_t)c * P + p) * T + t] = tot;
+  }
+}
+
+// --------------------------------------------------------- packed Shamir ----
+constexpr int kPssMaxK = 8;
+constexpr int kPssMaxT = 16;
+constexpr int kPssMaxN = 64;
+
+template <typename VT, int MASK>
+__global__ void __launch_bounds__(kBlock)
+    k_share_pss(int P, int D, int n, int k, int t, ModParams mp, int small_acc,
+                const int32_t* __restrict__ secrets, const uint32_t* __restrict__ mat,
+                RngKeyArg rng, uint64_t owner_base, VT* __restrict__ shares,
+                uint32_t* __restrict__ cnt, uint32_t* __restrict__ mask_out,
+                uint32_t* __restrict__ mask_cnt, const uint32_t* __restrict__ seeds,
+                int seed_words, uint32_t* err) {
+  __shared__ uint32_t sM[kPssMaxN * (kPssMaxK + kPssMaxT)];
+  __shared__ uint32_t scratch[kWaves];
+  const int K = k + t;
+  for (int i = threadIdx.x; i < n * K; i += kBlock) sM[i] = mat[i];
+  __syncthreads();
+  const int tile = blockIdx.x, p = blockIdx.y, T = gridDim.x;
+  const int tid = threadIdx.x;
+  const int B = (D + k - 1) / k;
+  const uint64_t owner = owner_base + (uint64_t)p;
+  const RngKey rk = to_key(rng);
+  const uint32_t m = mp.m;
+
+  uint32_t mask_bytes = 0;
+  uint32_t seedkey[8];
+  if constexpr (MASK == kMaskChaCha) load_seed_key(seedkey, seeds, p, seed_words);
+
+  // per-clerk byte counters live in LDS-free registers only for small n; use
+  // one pass per clerk group of 8 to bound registers.
+  for (int cg = 0; cg < n; cg += 8) {
+    uint32_t bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 16; ++i) {
+      const int b = tile * kTileValues + tid + kBlock * i;
+      if (b >= B) break;
+      uint32_t v[kPssMaxK + kPssMaxT];
+      // secrets (+mask) of this batch
+#pragma unroll
+      for (int j = 0; j < kPssMaxK; ++j) {
+        if (j < k) {
+          const int e = b * k + j;
+          uint32_t x = e < D ? canon_i32(secrets[(size_t)p * D + e], mp) : 0u;
+          if (e < D) {
+            if constexpr (MASK == kMaskFull) {
+              uint32_t w[16];
+              rng_block(w, rk, stream_id(kPurposeMaskFull, owner), (uint64_t)e / 16);
+              uint32_t mk = draw(w[e % 16], rk, kPurposeMaskRetry, owner, (uint64_t)e, mp);
+              x = add_mod(x, mk, m);
+              if (cg == 0) {
+                mask_out[(size_t)p * D + e] = mk;
+                mask_bytes += vlen(mk);
+              }
+            } else if constexpr (MASK == kMaskChaCha) {
+              uint32_t w[16];
+              chacharng_block(w, seedkey, (uint64_t)e / 8);
+              const int q = (e % 8) * 2;
+              uint64_t vv = ((uint64_t)w[q] << 32) | w[q + 1];
+              if (vv >= mp.zone64) atomicOr(err, kErrChaChaReject);
+              x = add_mod(x, mod64(vv, mp), m);
+            }
+          }
+          v[j] = x;
+        } else {
+          v[j] = 0;
+        }
+      }
+      // t uniform draws: one ChaCha block per batch
+      {
+        uint32_t w[16];
+        rng_block(w, rk, stream_id(kPurposeShares, owner), (uint64_t)b);
+#pragma unroll
+        for (int d = 0; d < kPssMaxT; ++d)
+          v[kPssMaxK + d] = d < t ? draw(w[d], rk, kPurposeSharesRetry, owner,
+                                         (uint64_t)b * 16 + d, mp)
+                                  : 0u;
+      }
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc) {
+        const int c = cg + cc;
+        if (c >= n) break;
+        const uint32_t* row = sM + c * K;
+        uint32_t y;
+        if (small_acc) {
+          uint64_t acc = 0;
+#pragma unroll
+          for (int j = 0; j < kPssMaxK; ++j)
+            if (j < k) acc += (uint64_t)row[j] * v[j];
+#pragma unroll
+          for (int d = 0; d < kPssMaxT; ++d)
+            if (d < t) acc += (uint64_t)row[k + d] * v[kPssMaxK + d];
+          y = mod64(acc, mp);
+        } else {
+          uint32_t acc = 0;
+#pragma unroll
+          for (int j = 0; j < kPssMaxK; ++j)
+            if (j < k) acc = add_mod(acc, mod64((uint64_t)row[j] * v[j], mp), m);
+#pragma unroll
+          for (int d = 0; d < kPssMaxT; ++d)
+            if (d < t) acc = add_mod(acc, mod64((uint64_t)row[k + d] * v[kPssMaxK + d], mp), m);
+          y = acc;
+        }
+        shares[((size_t)c * P + p) * B + b] = (VT)y;
+        bytes[cc] += vlen(y);
+      }
+    }
+    for (int cc = 0; cc < 8; ++cc) {
+      const int c = cg + cc;
+      if (c >= n) break;
+      uint32_t tot = block_sum(bytes[cc], scratch);
+      if (tid == 0) cnt[((size_t)c * P + p) * T + tile] = tot;
+    }
+  }
+  if constexpr (MASK == kMaskFull) {
+    // mask message tiles are over D elements with kTileValues per tile; the
+    // engine recounts them with k_count (PSS batches do not align with them).
+    (void)mask_bytes;
+    (void)mask_cnt;
+  }
+}
+
+// ----------------------------------------------------------------- count ---
+template <typename VT>
+__global__ void __launch_bounds__(kBlock) k_count(int L, const VT* __restrict__ vals,
+                                                  uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t scratch[kWaves];
+  const int t = blockIdx.x, j = blockIdx.y, T = gridDim.x;
+  const int e0 = t * kTileValues + threadIdx.x * 16;
+  const VT* src = vals + (size_t)j * L;
+  uint32_t bytes = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (e0 + i < L) bytes += vlen((uint32_t)src[e0 + i]);
+  uint32_t tot = block_sum(bytes, scratch);
+  if (threadIdx.x == 0) cnt[(size_t)j * T + t] = tot;
+}
+
+// ---------------------------------------------------- ChaCha mask (recipient)
+__global__ void __launch_bounds__(kBlock)
+    k_chacha_mask_sum(int P, int D, ModParams mp, int seed_words,
+                      const uint32_t* __restrict__ seeds, uint32_t* __restrict__ out,
+                      uint32_t* err) {
+  const int e0 = (blockIdx.x * kBlock + threadIdx.x) * 16;
+  if (e0 >= D) return;
+  uint64_t acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0;
+  for (int p = 0; p < P; ++p) {
+    uint32_t key[8], mk[16];
+    load_seed_key(key, seeds, p, seed_words);
+    chacha_mask16(mk, key, (uint64_t)e0, mp, err);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] += mk[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (e0 + i < D) out[e0 + i] = mod64(acc[i], mp);
+}
+
+}  // namespace
+
+void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, const int32_t* secrets,
+                           int mask_mode, int seed_words, RngKeyArg rng, uint64_t owner_base,
+                           void* shares, uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt,
+                           uint32_t* seeds, uint32_t* err, hipStream_t s) {
+  if (P <= 0 || D <= 0) return;
+  ModParams mp = make_mod_params(m);
+  if (mask_mode == kMaskChaCha)
+    hipLaunchKernelGGL(k_chacha_seeds, dim3((P + 63) / 64), dim3(64), 0, s, P, seed_words, rng,
+                       owner_base, seeds);
+  dim3 grid((D + kTileValues - 1) / kTileValues, P);
+#define SDA_ADD_LAUNCH(VT, MK)                                                                \
+  hipLaunchKernelGGL((k_share_additive<VT, MK>), grid, dim3(kBlock), 0, s, P, D, n, mp,        \
+                     secrets, rng, owner_base, (VT*)shares, cnt, mask_out, mask_cnt, seeds,    \
+                     seed_words, err)
+  if (value_bytes == 2) {
+    if (mask_mode == kMaskFull) SDA_ADD_LAUNCH(uint16_t, kMaskFull);
+    else if (mask_mode == kMaskChaCha) SDA_ADD_LAUNCH(uint16_t, kMaskChaCha);
+    else SDA_ADD_LAUNCH(uint16_t, kMaskNone);
+  } else {
+    if (mask_mode == kMaskFull) SDA_ADD_LAUNCH(uint32_t, kMaskFull);
+    else if (mask_mode == kMaskChaCha) SDA_ADD_LAUNCH(uint32_t, kMaskChaCha);
+    else SDA_ADD_LAUNCH(uint32_t, kMaskNone);
+  }
+#undef SDA_ADD_LAUNCH
+}
+
+void launch_share_pss(int P, int D, int n, int k, int t, uint32_t p, int value_bytes,
+                      const int32_t* secrets, const uint32_t* share_matrix, int mask_mode,
+                      int seed_words, RngKeyArg rng, uint64_t owner_base, void* shares,
+                      uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt, uint32_t* seeds,
+                      uint32_t* err, hipStream_t s) {
+  if (P <= 0 || D <= 0) return;
+  ModParams mp = make_mod_params(p);
+  const int B = (D + k - 1) / k;
+  // accumulate in u64 without intermediate reduction when K*(p-1)^2 < 2^64
+  const double bound = (double)(k + t) * (double)(p - 1) * (double)(p - 1);
+  const int small_acc = bound < 1.8e19 ? 1 : 0;
+  if (mask_mode == kMaskChaCha)
+    hipLaunchKernelGGL(k_chacha_seeds, dim3((P + 63) / 64), dim3(64), 0, s, P, seed_words, rng,
+                       owner_base, seeds);
+  dim3 grid((B + kTileValues - 1) / kTileValues, P);
+#define SDA_PSS_LAUNCH(VT, MK)                                                                \
+  hipLaunchKernelGGL((k_share_pss<VT, MK>), grid, dim3(kBlock), 0, s, P, D, n, k, t, mp,       \
+                     small_acc, secrets, share_matrix, rng, owner_base, (VT*)shares, cnt,      \
+                     mask_out, mask_cnt, seeds, seed_words, err)
+  if (value_bytes == 2) {
+    if (mask_mode == kMaskFull) SDA_PSS_LAUNCH(uint16_t, kMaskFull);
+    else if (mask_mode == kMaskChaCha) SDA_PSS_LAUNCH(uint16_t, kMaskChaCha);
+    else SDA_PSS_LAUNCH(uint16_t, kMaskNone);
+  } else {
+    if (mask_mode == kMaskFull) SDA_PSS_LAUNCH(uint32_t, kMaskFull);
+    else if (mask_mode == kMaskChaCha) SDA_PSS_LAUNCH(uint32_t, kMaskChaCha);
+    else SDA_PSS_LAUNCH(uint32_t, kMaskNone);
+  }
+#undef SDA_PSS_LAUNCH
+}
+
+void launch_count(int M, int L, int value_bytes, const void* vals, uint32_t* cnt, hipStream_t s) {
+  if (M <= 0 || L <= 0) return;
+  dim3 grid((L + kTileValues - 1) / kTileValues, M);
+  if (value_bytes == 2)
+    hipLaunchKernelGGL(k_count<uint16_t>, grid, dim3(kBlock), 0, s, L, (const uint16_t*)vals, cnt);
+  else
+    hipLaunchKernelGGL(k_count<uint32_t>, grid, dim3(kBlock), 0, s, L, (const uint32_t*)vals, cnt);
+}
+
+void launch_chacha_mask_sum(int P, int D, uint32_t m, int seed_words, const uint32_t* seeds,
+                            uint32_t* out, uint32_t* err, hipStream_t s) {
+  if (D <= 0) return;
+  ModParams mp = make_mod_params(m);
+  int threads = (D + 15) / 16;
+  hipLaunchKernelGGL(k_chacha_mask_sum, dim3((threads + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                     P, D, mp, seed_words, seeds, out, err);
+}
+
+}  // namespace sdagpu

@@ -1,0 +1,245 @@
+"""Checked, tensor-level wrappers around the gfx950 kernels in ``_sda_gpu``.
+
+Every wrapper validates device / dtype / shape / contiguity on the host before
+launching (a kernel fed a wrong shape could fault the whole node), then passes
+raw pointers plus the current HIP stream. All launches are asynchronous.
+"""
+from __future__ import annotations
+
+import torch
+
+from .._native import gpu as _gpu
+
+TILE_VALUES = 4096
+CHUNK_BYTES = 16384
+MSGKEY_BYTES = 80
+SEAL_OVERHEAD = 48
+
+MASK_NONE, MASK_FULL, MASK_CHACHA = 0, 1, 2
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: torch.Tensor) -> int:
+    return t.data_ptr()
+
+
+def _check(t: torch.Tensor, name: str, dtype=None, numel: int | None = None, min_numel: int | None = None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a GPU tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if dtype is not None and t.dtype not in (dtype if isinstance(dtype, tuple) else (dtype,)):
+        raise TypeError(f"{name}: dtype {t.dtype} not in {dtype}")
+    if numel is not None and t.numel() != numel:
+        raise ValueError(f"{name}: expected {numel} elements, got {t.numel()}")
+    if min_numel is not None and t.numel() < min_numel:
+        raise ValueError(f"{name}: expected at least {min_numel} elements, got {t.numel()}")
+
+
+def value_dtype(modulus: int) -> torch.dtype:
+    """u16 storage when every canonical value fits (m <= 65536), else u32 (int32 view)."""
+    return torch.int16 if 0 < modulus <= 65536 else torch.int32
+
+
+def value_bytes(dtype: torch.dtype) -> int:
+    return 2 if dtype == torch.int16 else 4
+
+
+def varint_max_len(modulus: int) -> int:
+    """Longest zigzag varint of a canonical value below `modulus` (0 = any u32)."""
+    if modulus == 0:
+        return 5
+    z = 2 * (modulus - 1)
+    n = 1
+    while z >= 128:
+        z >>= 7
+        n += 1
+    return n
+
+
+def tiles(L: int) -> int:
+    return (L + TILE_VALUES - 1) // TILE_VALUES
+
+
+def chunks_for(max_pt: int) -> int:
+    return (max_pt + 32 + CHUNK_BYTES - 1) // CHUNK_BYTES
+
+
+def rng_words(key: bytes) -> list[int]:
+    if len(key) != 32:
+        raise ValueError("rng key must be 32 bytes")
+    return [int.from_bytes(key[4 * i:4 * i + 4], "little") for i in range(8)]
+
+
+# --------------------------------------------------------------- launches ----
+def seal_setup(M, rng_key, owner_base, key_idx, pks, ct, stride, keys, err):
+    _check(key_idx, "key_idx", torch.int32, numel=M)
+    _check(pks, "pks", torch.int32)
+    if pks.numel() % 8:
+        raise ValueError("pks must be [K][8] words")
+    _check(ct, "ct", torch.uint8, min_numel=M * stride)
+    _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
+    _check(err, "err", torch.int32, numel=1)
+    if stride % 64:
+        raise ValueError("stride must be a multiple of 64")
+    _gpu().seal_setup(M, rng_words(rng_key), owner_base, _ptr(key_idx), _ptr(pks), _ptr(ct),
+                      stride, _ptr(keys), _ptr(err), _stream())
+
+
+def open_setup(M, key_idx, sks, pks, ct, stride, keys, err):
+    _check(key_idx, "key_idx", torch.int32, numel=M)
+    _check(sks, "sks", torch.int32)
+    _check(pks, "pks", torch.int32, numel=sks.numel())
+    _check(ct, "ct", torch.uint8, min_numel=M * stride)
+    _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
+    _check(err, "err", torch.int32, numel=1)
+    _gpu().open_setup(M, _ptr(key_idx), _ptr(sks), _ptr(pks), _ptr(ct), stride, _ptr(keys),
+                      _ptr(err), _stream())
+
+
+def x25519(scalars: torch.Tensor, points: torch.Tensor) -> torch.Tensor:
+    _check(scalars, "scalars", torch.int32)
+    _check(points, "points", torch.int32, numel=scalars.numel())
+    if scalars.numel() % 8:
+        raise ValueError("x25519 operands are [N][8] words")
+    out = torch.empty_like(scalars)
+    _gpu().x25519(scalars.numel() // 8, _ptr(scalars), _ptr(points), _ptr(out), _stream())
+    return out
+
+
+def share_additive(secrets, n, modulus, shares, cnt, mask_mode, rng_key, owner_base,
+                   mask_out=None, mask_cnt=None, seeds=None, seed_words=0, err=None):
+    P, D = secrets.shape
+    _check(secrets, "secrets", torch.int32)
+    vb = value_bytes(shares.dtype)
+    _check(shares, "shares", (torch.int16, torch.int32), numel=n * P * D)
+    T = tiles(D)
+    _check(cnt, "cnt", torch.int32, numel=n * P * T)
+    _check(err, "err", torch.int32, numel=1)
+    if n < 2:
+        raise ValueError("additive sharing needs at least 2 shares")
+    if mask_mode == MASK_FULL:
+        _check(mask_out, "mask_out", torch.int32, numel=P * D)
+        _check(mask_cnt, "mask_cnt", torch.int32, numel=P * T)
+    if mask_mode == MASK_CHACHA:
+        if not 1 <= seed_words <= 8:
+            raise ValueError("seed_words must be 1..8")
+        _check(seeds, "seeds", torch.int32, numel=P * seed_words)
+    z = 0
+    _gpu().share_additive(P, D, n, modulus, vb, _ptr(secrets), mask_mode, seed_words,
+                          rng_words(rng_key), owner_base, _ptr(shares), _ptr(cnt),
+                          _ptr(mask_out) if mask_out is not None else z,
+                          _ptr(mask_cnt) if mask_cnt is not None else z,
+                          _ptr(seeds) if seeds is not None else z, _ptr(err), _stream())
+
+
+def share_pss(secrets, n, k, t, prime, matrix, shares, cnt, mask_mode, rng_key, owner_base,
+              mask_out=None, seeds=None, seed_words=0, err=None):
+    P, D = secrets.shape
+    B = (D + k - 1) // k
+    _check(secrets, "secrets", torch.int32)
+    _check(matrix, "matrix", torch.int32, numel=n * (k + t))
+    vb = value_bytes(shares.dtype)
+    _check(shares, "shares", (torch.int16, torch.int32), numel=n * P * B)
+    _check(cnt, "cnt", torch.int32, numel=n * P * tiles(B))
+    _check(err, "err", torch.int32, numel=1)
+    if mask_mode == MASK_FULL:
+        _check(mask_out, "mask_out", torch.int32, numel=P * D)
+    if mask_mode == MASK_CHACHA:
+        _check(seeds, "seeds", torch.int32, numel=P * seed_words)
+    z = 0
+    _gpu().share_pss(P, D, n, k, t, prime, vb, _ptr(secrets), _ptr(matrix), mask_mode, seed_words,
+                     rng_words(rng_key), owner_base, _ptr(shares), _ptr(cnt),
+                     _ptr(mask_out) if mask_out is not None else z, z,
+                     _ptr(seeds) if seeds is not None else z, _ptr(err), _stream())
+
+
+def count(vals: torch.Tensor, cnt: torch.Tensor):
+    M, L = vals.shape
+    _check(vals, "vals", (torch.int16, torch.int32))
+    _check(cnt, "cnt", torch.int32, numel=M * tiles(L))
+    _gpu().count(M, L, value_bytes(vals.dtype), _ptr(vals), _ptr(cnt), _stream())
+
+
+def chacha_mask_sum(seeds: torch.Tensor, D: int, modulus: int, out: torch.Tensor, err):
+    P, w = seeds.shape
+    _check(seeds, "seeds", torch.int32)
+    _check(out, "out", torch.int32, numel=D)
+    _gpu().chacha_mask_sum(P, D, modulus, w, _ptr(seeds), _ptr(out), _ptr(err), _stream())
+
+
+def segscan(data: torch.Tensor, totals: torch.Tensor | None):
+    M, T = data.shape
+    _check(data, "data", torch.int32)
+    if totals is not None:
+        _check(totals, "totals", torch.int32, numel=M)
+    _gpu().segscan(M, T, _ptr(data), _ptr(totals) if totals is not None else 0, _stream())
+
+
+def encode_encrypt(vals, tile_off, keys, ct, stride):
+    M, L = vals.shape
+    _check(vals, "vals", (torch.int16, torch.int32))
+    _check(tile_off, "tile_off", torch.int32, numel=M * tiles(L))
+    _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
+    _check(ct, "ct", torch.uint8, min_numel=M * stride)
+    _gpu().encode_encrypt(M, L, value_bytes(vals.dtype), _ptr(vals), _ptr(tile_off), _ptr(keys),
+                          _ptr(ct), stride, _stream())
+
+
+def mac_chunks(M, K, keys, ct, stride, pt_len, partials, decrypt, term_cnt=None):
+    _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
+    _check(ct, "ct", torch.uint8, min_numel=M * stride)
+    _check(pt_len, "pt_len", torch.int32, numel=M)
+    _check(partials, "partials", torch.int32, numel=M * K * 8)
+    if decrypt:
+        _check(term_cnt, "term_cnt", torch.int32, numel=M * K)
+    _gpu().mac_chunks(M, K, _ptr(keys), _ptr(ct), stride, _ptr(pt_len), _ptr(partials),
+                      1 if decrypt else 0, _ptr(term_cnt) if term_cnt is not None else 0, _stream())
+
+
+def mac_final(M, K, keys, ct, stride, pt_len, partials, verify, ok=None, err=None):
+    _check(partials, "partials", torch.int32, numel=M * K * 8)
+    _check(err, "err", torch.int32, numel=1)
+    if ok is not None:
+        _check(ok, "ok", torch.int32, numel=M)
+    _gpu().mac_final(M, K, _ptr(keys), _ptr(ct), stride, _ptr(pt_len), _ptr(partials),
+                     1 if verify else 0, _ptr(ok) if ok is not None else 0, _ptr(err), _stream())
+
+
+def decode(M, K, L, modulus, pt, stride, pt_len, elem_start, vals, err):
+    _check(vals, "vals", (torch.int16, torch.int32), numel=M * L)
+    _check(elem_start, "elem_start", torch.int32, numel=M * K)
+    _check(pt, "pt", torch.uint8, min_numel=M * stride)
+    _gpu().decode(M, K, L, modulus, value_bytes(vals.dtype), _ptr(pt), stride, _ptr(pt_len),
+                  _ptr(elem_start), _ptr(vals), _ptr(err), _stream())
+
+
+def colsum(vals: torch.Tensor, modulus: int, out: torch.Tensor):
+    """out[g][l] = sum_r vals[g][r][l] mod m for vals [G][R][L]."""
+    G, R, L = vals.shape
+    _check(vals, "vals", (torch.int16, torch.int32))
+    _check(out, "out", torch.int32, numel=G * L)
+    _gpu().colsum(G, R, L, modulus, value_bytes(vals.dtype), _ptr(vals), _ptr(out), _stream())
+
+
+def pss_reconstruct(ys: torch.Tensor, lag: torch.Tensor, k: int, D: int, prime: int,
+                    out: torch.Tensor):
+    nI, B = ys.shape
+    _check(ys, "ys", torch.int32)
+    _check(lag, "lag", torch.int32, numel=k * nI)
+    _check(out, "out", torch.int32, numel=D)
+    if B * k < D:
+        raise ValueError("not enough batches for the dimension")
+    _gpu().pss_reconstruct(B, k, nI, D, prime, _ptr(lag), _ptr(ys), _ptr(out), _stream())
+
+
+def sub_mod(a: torch.Tensor, b: torch.Tensor, modulus: int, out: torch.Tensor):
+    _check(a, "a", torch.int32)
+    _check(b, "b", torch.int32, numel=a.numel())
+    _check(out, "out", torch.int32, numel=a.numel())
+    _gpu().sub_mod(a.numel(), modulus, _ptr(a), _ptr(b), _ptr(out), _stream())

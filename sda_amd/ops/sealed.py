@@ -1,0 +1,132 @@
+"""Device sealed-box pipelines over a ciphertext *arena*.
+
+A message is a libsodium sealed box over the zigzag-varint encoding of a vector
+of field values -- exactly the `Encryption::Sodium` payload of the reference
+(client/src/crypto/encryption/sodium.rs:36-43 / 78-89). The arena stores M such
+messages in fixed 64-byte-aligned slots::
+
+    slot j: epk(32) | mac(16) | ciphertext (pt_len[j] bytes) | padding
+
+so the participant kernels can write without a length pre-pass, and a slot's
+bytes ``[0, 48 + pt_len[j])`` are a wire-format `Encryption` blob.
+
+``seal``  : counts -> tile offsets -> (X25519/BLAKE2b/HSalsa20 setup) -> varint
+            encode + XSalsa20 -> parallel Poly1305 -> header tag
+``open_`` : setup -> Poly1305 verify fused with in-place decryption and
+            terminator counting -> element ranks -> parallel varint decode
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import gpu as G
+
+
+def _round_up(x: int, a: int) -> int:
+    return (x + a - 1) // a * a
+
+
+@dataclass
+class Arena:
+    M: int
+    L: int
+    modulus: int
+    stride: int
+    K: int
+    ct: torch.Tensor      # uint8 [M * stride]
+    pt_len: torch.Tensor  # int32 [M]
+
+    @staticmethod
+    def slot_stride(L: int, modulus: int) -> int:
+        return _round_up(G.SEAL_OVERHEAD + _round_up(L * G.varint_max_len(modulus), 16), 64)
+
+    @classmethod
+    def empty(cls, M: int, L: int, modulus: int, device=None) -> "Arena":
+        device = device or torch.device("cuda")
+        stride = cls.slot_stride(L, modulus)
+        K = G.chunks_for(L * G.varint_max_len(modulus))
+        return cls(M, L, modulus, stride, K,
+                   torch.empty(M * stride, dtype=torch.uint8, device=device),
+                   torch.zeros(M, dtype=torch.int32, device=device))
+
+    # ---- host interop (wire-format blobs) --------------------------------
+    def to_blobs(self) -> list[bytes]:
+        lens = self.pt_len.cpu().tolist()
+        raw = self.ct.view(self.M, self.stride).cpu()
+        return [bytes(raw[j, :G.SEAL_OVERHEAD + lens[j]].numpy().tobytes()) for j in range(self.M)]
+
+    @classmethod
+    def from_blobs(cls, blobs: list[bytes], L: int, modulus: int, device=None) -> "Arena":
+        """Upload wire blobs (e.g. host- or reference-sealed) into an arena."""
+        device = device or torch.device("cuda")
+        maxpt = max([len(b) - G.SEAL_OVERHEAD for b in blobs] + [0])
+        stride = max(cls.slot_stride(L, modulus), _round_up(G.SEAL_OVERHEAD + _round_up(maxpt, 16), 64))
+        K = G.chunks_for(maxpt)
+        host = torch.zeros(len(blobs), stride, dtype=torch.uint8)
+        lens = []
+        for j, b in enumerate(blobs):
+            if len(b) < G.SEAL_OVERHEAD:
+                raise ValueError("blob shorter than a sealed-box header")
+            host[j, :len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+            lens.append(len(b) - G.SEAL_OVERHEAD)
+        return cls(len(blobs), L, modulus, stride, K, host.reshape(-1).to(device),
+                   torch.tensor(lens, dtype=torch.int32, device=device))
+
+    def slice(self, first: int, count: int) -> "Arena":
+        """View of messages [first, first+count) (no copy)."""
+        return Arena(count, self.L, self.modulus, self.stride, self.K,
+                     self.ct[first * self.stride:(first + count) * self.stride],
+                     self.pt_len[first:first + count])
+
+
+def seal(values: torch.Tensor, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: bytes,
+         owner_base: int, err: torch.Tensor, modulus: int, cnt: torch.Tensor | None = None,
+         arena: Arena | None = None) -> Arena:
+    """Seal each row of `values` [M][L] for public key pks[key_idx[row]]."""
+    M, L = values.shape
+    dev = values.device
+    if arena is None:
+        arena = Arena.empty(M, L, modulus, dev)
+    T = G.tiles(L)
+    if cnt is None:
+        cnt = torch.empty(M, T, dtype=torch.int32, device=dev)
+        G.count(values, cnt)
+    else:
+        cnt = cnt.view(M, T)
+    G.segscan(cnt, arena.pt_len)  # cnt becomes the tile byte offsets
+    keys = torch.empty(M * G.MSGKEY_BYTES, dtype=torch.uint8, device=dev)
+    G.seal_setup(M, rng_key, owner_base, key_idx, pks, arena.ct, arena.stride, keys, err)
+    G.encode_encrypt(values, cnt, keys, arena.ct, arena.stride)
+    partials = torch.empty(M * arena.K * 8, dtype=torch.int32, device=dev)
+    G.mac_chunks(M, arena.K, keys, arena.ct, arena.stride, arena.pt_len, partials, decrypt=False)
+    G.mac_final(M, arena.K, keys, arena.ct, arena.stride, arena.pt_len, partials, verify=False,
+                err=err)
+    return arena
+
+
+def open_(arena: Arena, key_idx: torch.Tensor, sks: torch.Tensor, pks: torch.Tensor,
+          err: torch.Tensor, out_dtype: torch.dtype | None = None,
+          out: torch.Tensor | None = None) -> torch.Tensor:
+    """Verify + decrypt (in place) + decode every message; returns [M][L] values.
+
+    Destroys the ciphertext (it is replaced by plaintext).
+    """
+    M, L, K = arena.M, arena.L, arena.K
+    dev = arena.ct.device
+    keys = torch.empty(M * G.MSGKEY_BYTES, dtype=torch.uint8, device=dev)
+    G.open_setup(M, key_idx, sks, pks, arena.ct, arena.stride, keys, err)
+    partials = torch.empty(M * K * 8, dtype=torch.int32, device=dev)
+    term = torch.empty(M, K, dtype=torch.int32, device=dev)
+    G.mac_chunks(M, K, keys, arena.ct, arena.stride, arena.pt_len, partials, decrypt=True,
+                 term_cnt=term)
+    G.mac_final(M, K, keys, arena.ct, arena.stride, arena.pt_len, partials, verify=True, err=err)
+    totals = torch.empty(M, dtype=torch.int32, device=dev)
+    G.segscan(term, totals)
+    # exactly L values per message, otherwise malformed
+    err.bitwise_or_((totals != L).any().to(torch.int32) * 4)
+    if out is None:
+        out = torch.empty(M, L, dtype=out_dtype or G.value_dtype(arena.modulus), device=dev)
+    G.decode(M, K, L, arena.modulus, arena.ct, arena.stride, arena.pt_len, term, out, err)
+    return out

@@ -1,0 +1,183 @@
+"""GPU kernel numerics: every HIP kernel against the host C++ oracle or a plain
+PyTorch reference of the same op (run with -m gpu on an MI355X)."""
+import os
+
+import pytest
+import torch
+
+from helpers import varint_decode, varint_encode
+
+pytestmark = pytest.mark.gpu
+
+
+def _words_le(b: bytes):
+    return [int.from_bytes(b[4 * i:4 * i + 4], "little", signed=True) for i in range(len(b) // 4)]
+
+
+def _bytes_le(words):
+    return b"".join((int(w) & 0xFFFFFFFF).to_bytes(4, "little") for w in words)
+
+
+def test_x25519_matches_host(cuda, native):
+    c = native.crypto
+    N = 96
+    sc = [os.urandom(32) for _ in range(N)]
+    pts = [c.box_keypair()[0] for _ in range(N - 2)] + [bytes([9] + [0] * 31), os.urandom(32)]
+    from sda_amd.ops import gpu as G
+    out = G.x25519(torch.tensor([_words_le(s) for s in sc], dtype=torch.int32, device=cuda),
+                   torch.tensor([_words_le(p) for p in pts], dtype=torch.int32, device=cuda))
+    out = out.cpu().tolist()
+    for i in range(N):
+        assert _bytes_le(out[i]) == c.x25519(sc[i], pts[i])[0], i
+
+
+def _keytable(native, cuda, count):
+    from sda_amd.engine import KeyTable
+    return KeyTable.generate(count, cuda)
+
+
+@pytest.mark.parametrize("L,modulus", [(1, 433), (10, 433), (5000, 433), (20000, 433),
+                                       (3000, 2 ** 31 - 1), (70000, 65521)])
+def test_gpu_seal_opens_on_host(cuda, native, L, modulus):
+    from sda_amd.ops import gpu as G
+    from sda_amd.ops.sealed import seal
+    keys = _keytable(native, cuda, 2)
+    M = 5
+    vdt = G.value_dtype(modulus)
+    vals64 = torch.randint(0, modulus, (M, L), dtype=torch.int64)
+    vals = vals64.to(vdt).to(cuda) if vdt == torch.int16 else vals64.to(torch.int32).to(cuda)
+    kidx = torch.tensor([j % 2 for j in range(M)], dtype=torch.int32, device=cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    arena = seal(vals, kidx, keys.pks, os.urandom(32), 0, err, modulus)
+    blobs = arena.to_blobs()
+    assert int(err.item()) == 0
+    for j in range(M):
+        pk, sk = keys.pk_bytes[j % 2], keys.sk_bytes[j % 2]
+        pt = native.crypto.box_seal_open(blobs[j], pk, sk)
+        assert pt is not None, f"host could not open GPU box {j}"
+        assert varint_decode(pt) == vals64[j].tolist()
+
+
+@pytest.mark.parametrize("L", [1, 7, 4096, 9000, 40000])
+def test_host_seal_opens_on_gpu(cuda, native, L):
+    """Host (libsodium-format) boxes, including Rust-style negative shares."""
+    from sda_amd.ops.sealed import Arena, open_
+    m = 433
+    keys = _keytable(native, cuda, 1)
+    M = 4
+    rows = []
+    blobs = []
+    for j in range(M):
+        row = [int(x) for x in torch.randint(-m + 1, m, (L,)).tolist()]
+        rows.append([x % m for x in row])
+        blobs.append(native.crypto.box_seal(varint_encode(row), keys.pk_bytes[0]))
+    arena = Arena.from_blobs(blobs, L, m, cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    kidx = torch.zeros(M, dtype=torch.int32, device=cuda)
+    out = open_(arena, kidx, keys.sks, keys.pks, err, out_dtype=torch.int32)
+    assert int(err.item()) == 0
+    assert out.cpu().tolist() == rows
+
+
+def test_tampered_box_is_rejected(cuda, native):
+    from sda_amd.ops.sealed import Arena, open_
+    keys = _keytable(native, cuda, 1)
+    blob = bytearray(native.crypto.box_seal(varint_encode(list(range(100))), keys.pk_bytes[0]))
+    blob[60] ^= 0x10
+    arena = Arena.from_blobs([bytes(blob)], 100, 433, cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    open_(arena, torch.zeros(1, dtype=torch.int32, device=cuda), keys.sks, keys.pks, err)
+    assert int(err.item()) & 2
+
+
+def test_colsum_matches_torch(cuda):
+    from sda_amd.ops import gpu as G
+    for dt, m in [(torch.int16, 433), (torch.int32, 2 ** 31 - 1)]:
+        x = torch.randint(0, m, (3, 50, 1003), dtype=torch.int64)
+        out = torch.empty(3, 1003, dtype=torch.int32, device=cuda)
+        G.colsum(x.to(dt).to(cuda) if dt == torch.int16 else x.to(torch.int32).to(cuda), m, out)
+        assert torch.equal(out.cpu().to(torch.int64), x.sum(1) % m)
+
+
+def test_chacha_mask_matches_rand03(cuda, native):
+    from sda_amd.ops import gpu as G
+    P, D, m = 3, 50, 433
+    seeds = torch.randint(-2 ** 31, 2 ** 31, (P, 4), dtype=torch.int64).to(torch.int32)
+    out = torch.empty(D, dtype=torch.int32, device=cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    G.chacha_mask_sum(seeds.to(cuda), D, m, out, err)
+    exp = [0] * D
+    for p in range(P):
+        rng = native.crypto.ChaChaRng([int(w) & 0xFFFFFFFF for w in seeds[p].tolist()])
+        for i in range(D):
+            exp[i] = (exp[i] + rng.gen_range(0, m)) % m
+    assert out.cpu().tolist() == exp
+    assert int(err.item()) == 0
+
+
+def test_additive_shares_sum_to_secret(cuda):
+    from sda_amd.ops import gpu as G
+    P, D, n, m = 4, 5000, 3, 433
+    secrets = torch.randint(-1000, 1000, (P, D), dtype=torch.int32, device=cuda)
+    shares = torch.empty(n, P, D, dtype=torch.int16, device=cuda)
+    cnt = torch.empty(n * P * G.tiles(D), dtype=torch.int32, device=cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    G.share_additive(secrets, n, m, shares, cnt, G.MASK_NONE, os.urandom(32), 0, err=err)
+    s = shares.to(torch.int64).sum(0) % m
+    assert torch.equal(s, torch.remainder(secrets.to(torch.int64), m))
+    # random shares are spread over [0, m)
+    r = shares[0].to(torch.int64).flatten()
+    assert r.min() >= 0 and r.max() < m
+    hist = torch.bincount(r, minlength=m).float()
+    assert hist.std() / hist.mean() < 0.25
+    # byte counts match the varint lengths
+    exp = [len(varint_encode(shares[c, p].to(torch.int64).tolist())) for c in range(n) for p in range(P)]
+    got = cnt.view(n * P, -1).sum(1).tolist()
+    assert got == exp
+
+
+def _round(cuda, spec, P, clerks=None):
+    from sda_amd.engine import DeviceAggregator, reference_sum
+    agg = DeviceAggregator(spec, cuda)
+    secrets = torch.randint(0, spec.field_modulus, (P, spec.dimension), dtype=torch.int32,
+                            device=cuda)
+    res = agg.run_round(secrets, clerks=clerks)
+    assert torch.equal(res.output, reference_sum(secrets, spec.field_modulus))
+    return res
+
+
+def test_round_additive(cuda):
+    from sda_amd.models import AggregationSpec, Additive
+    _round(cuda, AggregationSpec(10000, 433, Additive(3, 433)), 7)
+
+
+def test_round_additive_fullmask(cuda):
+    from sda_amd.models import AggregationSpec, Additive, FullMask
+    _round(cuda, AggregationSpec(5000, 433, Additive(3, 433), FullMask(433)), 5)
+
+
+def test_round_additive_chachamask(cuda):
+    from sda_amd.models import AggregationSpec, Additive, ChaChaMask
+    _round(cuda, AggregationSpec(5000, 433, Additive(3, 433), ChaChaMask(433, 5000)), 5)
+
+
+def test_round_large_modulus(cuda):
+    from sda_amd.models import AggregationSpec, Additive
+    m = 2 ** 31 - 1
+    _round(cuda, AggregationSpec(3000, m, Additive(5, m)), 4)
+
+
+def test_round_pss_483(cuda):
+    from sda_amd.models import AggregationSpec, PSS_4_8_3
+    _round(cuda, AggregationSpec(10000, 433, PSS_4_8_3), 6)
+
+
+def test_round_pss_dropout(cuda):
+    from sda_amd.models import AggregationSpec, PSS_4_8_3, pss_5_of_8
+    _round(cuda, AggregationSpec(3001, 433, PSS_4_8_3), 4, clerks=[0, 1, 2, 4, 5, 6, 7])
+    _round(cuda, AggregationSpec(3001, 433, pss_5_of_8()), 4, clerks=[1, 3, 4, 6, 7])
+
+
+def test_round_pss_fullmask(cuda):
+    from sda_amd.models import AggregationSpec, PSS_4_8_3, FullMask
+    _round(cuda, AggregationSpec(2000, 433, PSS_4_8_3, FullMask(433)), 3)
