@@ -87,3 +87,11 @@ asan:
 
 clean:
 	rm -rf $(BUILD) $(LIB)/*.so $(BIN)
+
+# host emulation of the device algorithms (no GPU needed)
+emul: $(BUILD)/hip/host_emul
+	$(BUILD)/hip/host_emul
+$(BUILD)/hip/host_emul: csrc/kernels/host_emul.cpp $(wildcard csrc/kernels/*.hpp) $(CORE_LIB)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -O2 -std=c++17 --offload-arch=$(GPU_ARCH) $(INCS) -c $< -o $@.o
+	$(HIPCC) --offload-arch=$(GPU_ARCH) $@.o $(CORE_LIB) -o $@ -pthread

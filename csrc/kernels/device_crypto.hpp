@@ -15,7 +15,7 @@
 
 #include <cstdint>
 
-#define SDA_DEV __device__ __forceinline__
+#define SDA_DEV __host__ __device__ __forceinline__
 
 namespace sdagpu {
 

@@ -261,7 +261,6 @@ __global__ void __launch_bounds__(64)
     }
     prev = e;
   }
-  H = p130_mul(H, r);
   const uint32_t s4[4] = {key.poly_s[0], key.poly_s[1], key.poly_s[2], key.poly_s[3]};
   uint32_t tag[4];
   p130_finish(tag, H, s4);
