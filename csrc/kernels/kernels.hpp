@@ -28,7 +28,8 @@ struct MsgKey {
 };
 static_assert(sizeof(MsgKey) == 80, "MsgKey layout");
 
-constexpr int kTileValues = 4096;   // values per encode tile (256 threads x 16)
+constexpr int kTileValues = 4096;    // values per byte-count tile (256 lanes x 16)
+constexpr int kEncodeValues = 8192;  // values per encode tile = 2 count tiles (256 x 32)
 constexpr int kChunkBytes = 16384;  // bytes per MAC / decrypt chunk (256 threads x 64)
 
 // Error bits (device error word)

@@ -40,8 +40,9 @@ SDA_DEV uint32_t mod32(uint32_t w, const ModParams& P) {
 }
 SDA_DEV uint32_t mod64(uint64_t v, const ModParams& P) {
   uint64_t q = __umul64hi(v, P.mu64);
-  uint64_t r = v - q * (uint64_t)P.m;
-  while (r >= P.m) r -= P.m;
+  uint64_t r = v - q * (uint64_t)P.m;  // q >= floor(v/m) - 2
+  r = r >= P.m ? r - P.m : r;
+  r = r >= P.m ? r - P.m : r;
   return (uint32_t)r;
 }
 SDA_DEV uint32_t add_mod(uint32_t a, uint32_t b, uint32_t m) {

@@ -19,12 +19,38 @@
 namespace sdagpu {
 namespace {
 
+// Canonical field value of a decoded zigzag varint (general path handles
+// negative / oversized values from foreign encoders such as the reference's
+// Rust-`%` shares, which can be negative: additive.rs:47).
+SDA_DEV uint32_t canon_varint(uint64_t z, const ModParams& mp, bool& bad) {
+  if (!(z & 1)) {
+    const uint64_t mag = z >> 1;
+    if (mp.m == 0) {
+      bad |= mag > 0xffffffffULL;
+      return (uint32_t)mag;
+    }
+    return mag < mp.m ? (uint32_t)mag : mod64(mag, mp);
+  }
+  if (mp.m == 0) {
+    bad = true;
+    return 0;
+  }
+  const uint32_t r = mod64((z >> 1) + 1, mp);  // value = -(z>>1) - 1
+  return r == 0 ? 0u : mp.m - r;
+}
+
+// One block per (chunk, message). Each lane owns 64 plaintext bytes held in
+// registers; terminator positions are a 64-bit mask (popcount -> block scan ->
+// ranks), the varint straddling into a lane is carried in by looking back <= 9
+// bytes in LDS, and decoded values are staged in LDS so the global store of the
+// chunk's contiguous element range is coalesced.
 template <typename VT>
 __global__ void __launch_bounds__(kBlock)
     k_decode(int L, ModParams mp, const uint8_t* __restrict__ pt, uint64_t stride,
              const uint32_t* __restrict__ pt_len, const uint32_t* __restrict__ elem_start,
              VT* __restrict__ vals, uint32_t* err) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kChunkBytes + 16];
+  __shared__ VT outb[kChunkBytes];
   __shared__ uint32_t scratch[kWaves];
   const int k = blockIdx.x, j = blockIdx.y, K = gridDim.x;
   const int tid = threadIdx.x;
@@ -34,67 +60,71 @@ __global__ void __launch_bounds__(kBlock)
   const int64_t end = min((int64_t)N, kC + kChunkBytes - 32);
   if (start >= end) return;
   const uint8_t* gmsg = pt + (size_t)j * stride + 48;
-  // LDS image: index 16 + (pos - (kC - 32)); prefix [0,16) = 16 bytes before the chunk
-  const int64_t base = kC - 48;
+  const int64_t p0 = kC - 32 + 64 * tid;  // message position of this lane's first byte
+  uint32_t w[16];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int off = 64 * tid + 16 * q;
-    const int64_t pos = kC - 32 + off;
-    if (pos >= 0 && pos < end)
-      *reinterpret_cast<uint4*>(buf + 16 + off) = *reinterpret_cast<const uint4*>(gmsg + pos);
+    const int64_t pos = p0 + 16 * q;
+    uint4 d = make_uint4(0, 0, 0, 0);
+    if (pos >= 0 && pos < end) d = *reinterpret_cast<const uint4*>(gmsg + pos);
+    *reinterpret_cast<uint4*>(buf + 16 + 64 * tid + 16 * q) = d;
+    w[4 * q] = d.x; w[4 * q + 1] = d.y; w[4 * q + 2] = d.z; w[4 * q + 3] = d.w;
   }
-  if (tid == 0 && base >= 0)
-    *reinterpret_cast<uint4*>(buf) = *reinterpret_cast<const uint4*>(gmsg + base);
-  __syncthreads();
-  // rank terminators
-  uint32_t cnt = 0;
-  for (int b = 0; b < 64; ++b) {
-    const int64_t pos = kC - 32 + 64 * tid + b;
-    if (pos >= start && pos < end && !(buf[16 + 64 * tid + b] & 0x80)) ++cnt;
+  if (tid == 0 && kC - 48 >= 0)
+    *reinterpret_cast<uint4*>(buf) = *reinterpret_cast<const uint4*>(gmsg + kC - 48);
+  // valid bytes [lo, hi) of this lane
+  const int lo = (int)max((int64_t)0, start - p0);
+  const int hi = (int)min((int64_t)64, end - p0);
+  uint64_t vmask = 0;
+  if (hi > lo) {
+    const uint64_t upto = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
+    vmask = upto & ~((1ull << lo) - 1);
   }
-  uint32_t tot;
-  uint32_t rank = elem_start[(size_t)j * K + k] + block_excl_scan(cnt, scratch, &tot);
-  VT* out = vals + (size_t)j * L;
+  uint64_t tmask = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t t = ~w[i] & 0x80808080u;
+    const uint64_t bits = ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+    tmask |= bits << (4 * i);
+  }
+  tmask &= vmask;
+  uint32_t total;
+  uint32_t local = block_excl_scan((uint32_t)__popcll(tmask), scratch, &total);  // syncs
   bool bad = false;
+  uint64_t acc = 0;
+  uint32_t shift = 0;
+  if (vmask) {
+    // carry-in: continuation bytes right before this lane's first valid byte
+    const int64_t s = p0 + lo;
+    int n = 0;
+    while (n < 10 && s - n - 1 >= 0 && (buf[16 + (s - n - 1) - (kC - 32)] & 0x80)) ++n;
+    bad |= n >= 10;
+    for (int u = 0; u < n && u < 9; ++u) {
+      acc |= (uint64_t)(buf[16 + (s - n + u) - (kC - 32)] & 0x7f) << shift;
+      shift += 7;
+    }
+  }
+#pragma unroll
   for (int b = 0; b < 64; ++b) {
-    const int64_t pos = kC - 32 + 64 * tid + b;
-    if (pos < start || pos >= end) continue;
-    const uint32_t byte = buf[16 + 64 * tid + b];
-    if (byte & 0x80) {
-      if (pos == (int64_t)N - 1) bad = true;  // dangling continuation byte
-      continue;
-    }
-    // find the first byte of this varint
-    int64_t s = pos;
-    int steps = 0;
-    while (s > 0 && steps < 10 && (buf[16 + (s - 1) - (kC - 32)] & 0x80)) {
-      --s;
-      ++steps;
-    }
-    if (steps >= 10) { bad = true; ++rank; continue; }
-    uint64_t z = 0;
-    for (int64_t u = s; u <= pos; ++u) z |= (uint64_t)(buf[16 + u - (kC - 32)] & 0x7f) << (7 * (u - s));
-    // unzigzag, canonicalise
-    uint32_t val;
-    if (!(z & 1)) {
-      uint64_t mag = z >> 1;
-      if (mp.m == 0) {
-        if (mag > 0xffffffffULL) bad = true;
-        val = (uint32_t)mag;
-      } else {
-        val = mag < mp.m ? (uint32_t)mag : mod64(mag, mp);
-      }
-    } else {
-      uint64_t mag = (z >> 1) + 1;  // value = -mag
-      if (mp.m == 0) { bad = true; val = 0; }
-      else {
-        uint32_t r = mod64(mag, mp);
-        val = r == 0 ? 0u : mp.m - r;
+    if ((vmask >> b) & 1) {
+      const uint32_t byte = (w[b >> 2] >> (8 * (b & 3))) & 0xffu;
+      if (shift < 64) acc |= (uint64_t)(byte & 0x7f) << shift;
+      shift += 7;
+      if (!(byte & 0x80)) {
+        bad |= shift > 70;
+        outb[local++] = (VT)canon_varint(acc, mp, bad);
+        acc = 0;
+        shift = 0;
       }
     }
-    if (rank < (uint32_t)L) out[rank] = (VT)val;
+  }
+  if (p0 + hi == (int64_t)N && hi > lo && shift != 0) bad = true;  // dangling continuation
+  __syncthreads();
+  const uint32_t base = elem_start[(size_t)j * K + k];
+  VT* out = vals + (size_t)j * L;
+  for (uint32_t i = tid; i < total; i += kBlock) {
+    if (base + i < (uint32_t)L) out[base + i] = outb[i];
     else bad = true;
-    ++rank;
   }
   if (bad) atomicOr(err, kErrMalformed);
 }

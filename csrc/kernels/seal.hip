@@ -18,43 +18,77 @@
 namespace sdagpu {
 namespace {
 
-constexpr int kLdsEncodeBytes = kTileValues * 5 + 128;
+constexpr int kLdsEncodeBytes = kEncodeValues * 5 + 128;
+constexpr int kValuesPerLane = kEncodeValues / kBlock;  // 32
 
+template <typename VT>
+SDA_DEV void load_values(uint32_t (&v)[kValuesPerLane], const VT* src, int e0, int L, bool vec_ok) {
+  if (vec_ok && e0 + kValuesPerLane <= L) {
+    if constexpr (sizeof(VT) == 2) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 d = reinterpret_cast<const uint4*>(src + e0)[q];
+        const uint32_t ws[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[8 * q + 2 * u] = ws[u] & 0xffffu;
+          v[8 * q + 2 * u + 1] = ws[u] >> 16;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint4 d = reinterpret_cast<const uint4*>(src + e0)[q];
+        v[4 * q] = d.x; v[4 * q + 1] = d.y; v[4 * q + 2] = d.z; v[4 * q + 3] = d.w;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kValuesPerLane; ++i) v[i] = (e0 + i < L) ? (uint32_t)src[e0 + i] : 0u;
+  }
+}
+
+// One block per (tile of kEncodeValues values, message): lanes varint-encode 32
+// values each into LDS at scanned offsets, every lane then XORs (about) one
+// 64-byte XSalsa20 block in place, and the tile is stored with 16-byte writes
+// (byte writes only at the two tile edges shared with neighbouring tiles).
 template <typename VT>
 __global__ void __launch_bounds__(kBlock)
     k_encode_encrypt(int L, const VT* __restrict__ vals, const uint32_t* __restrict__ tile_off,
                      const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct, uint64_t stride) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEncodeBytes];
   __shared__ uint32_t scratch[kWaves];
-  const int t = blockIdx.x, j = blockIdx.y, T = gridDim.x;
+  const int t = blockIdx.x, j = blockIdx.y;
+  const int T = (L + kTileValues - 1) / kTileValues;  // count tiles per message
   const int tid = threadIdx.x;
-  const int e0 = t * kTileValues + tid * 16;
+  const int e0 = t * kEncodeValues + tid * kValuesPerLane;
   const VT* src = vals + (size_t)j * L;
-  uint32_t v[16];
+  const bool vec_ok = ((size_t)L * sizeof(VT)) % 16 == 0;
+  uint32_t v[kValuesPerLane];
+  load_values<VT>(v, src, e0, L, vec_ok);
   uint32_t my_bytes = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    v[i] = (e0 + i < L) ? (uint32_t)src[e0 + i] : 0u;
-    if (e0 + i < L) {
-      uint64_t z = (uint64_t)v[i] << 1;
-      my_bytes += 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
-    }
+  for (int i = 0; i < kValuesPerLane; ++i) {
+    const uint64_t z = (uint64_t)v[i] << 1;
+    const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
+    my_bytes += (e0 + i < L) ? len : 0u;
   }
   uint32_t tile_bytes;
   const uint32_t excl = block_excl_scan(my_bytes, scratch, &tile_bytes);
-  const uint32_t a = tile_off[(size_t)j * T + t];
+  const uint32_t a = tile_off[(size_t)j * T + t * (kEncodeValues / kTileValues)];
   const uint32_t b0 = (32u + a) >> 6;
   const uint32_t base = 32u + a - 64u * b0;  // LDS index of message byte `a`
   uint32_t pos = base + excl;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < kValuesPerLane; ++i) {
     if (e0 + i < L) {
-      uint64_t z = (uint64_t)v[i] << 1;
-      for (;;) {
-        uint8_t byte = (uint8_t)(z & 0x7f);
-        z >>= 7;
-        if (z) { lds[pos++] = byte | 0x80; } else { lds[pos++] = byte; break; }
-      }
+      const uint64_t z = (uint64_t)v[i] << 1;
+      const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
+#pragma unroll
+      for (int q = 0; q < 5; ++q)
+        if ((uint32_t)q < len)
+          lds[pos + q] = (uint8_t)(((z >> (7 * q)) & 0x7f) | ((uint32_t)q + 1 < len ? 0x80u : 0u));
+      pos += len;
     }
   }
   __syncthreads();
@@ -79,7 +113,7 @@ __global__ void __launch_bounds__(kBlock)
       *reinterpret_cast<uint4*>(gmsg + c) = *reinterpret_cast<const uint4*>(lds + (c - a + base));
     } else {
       for (uint32_t q = 0; q < 16; ++q) {
-        uint32_t p = c + q;
+        const uint32_t p = c + q;
         if (p >= a && p < end) gmsg[p] = lds[p - a + base];
       }
     }
@@ -288,7 +322,7 @@ void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
                            const uint32_t* tile_off, const MsgKey* keys, uint8_t* ct,
                            uint64_t stride, hipStream_t s) {
   if (M <= 0 || L <= 0) return;
-  dim3 grid((L + kTileValues - 1) / kTileValues, M);
+  dim3 grid((L + kEncodeValues - 1) / kEncodeValues, M);
   if (value_bytes == 2)
     hipLaunchKernelGGL(k_encode_encrypt<uint16_t>, grid, dim3(kBlock), 0, s, L,
                        (const uint16_t*)vals, tile_off, keys, ct, stride);

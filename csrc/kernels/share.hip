@@ -85,14 +85,14 @@ SDA_DEV void chacharng_block(uint32_t (&w)[16], const uint32_t (&key)[8], uint64
 // ChaCha mask for 16 consecutive elements starting at e0 (e0 % 8 == 0).
 SDA_DEV void chacha_mask16(uint32_t (&mk)[16], const uint32_t (&key)[8], uint64_t e0,
                            const ModParams& mp, uint32_t* err) {
-  uint32_t w[16];
   bool rej = false;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
+    uint32_t w[16];
     chacharng_block(w, key, e0 / 8 + half);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      uint64_t v = ((uint64_t)w[2 * i] << 32) | w[2 * i + 1];
+      const uint64_t v = ((uint64_t)w[2 * i] << 32) | w[2 * i + 1];
       rej |= v >= mp.zone64;
       mk[8 * half + i] = mod64(v, mp);
     }
@@ -100,9 +100,11 @@ SDA_DEV void chacha_mask16(uint32_t (&mk)[16], const uint32_t (&key)[8], uint64_
   if (rej) atomicOr(err, kErrChaChaReject);
 }
 
+// `p` is wave-uniform at every call site: keep the key in SGPRs.
 SDA_DEV void load_seed_key(uint32_t (&key)[8], const uint32_t* seeds, int p, int seed_words) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) key[i] = i < seed_words ? seeds[(size_t)p * seed_words + i] : 0u;
+  for (int i = 0; i < 8; ++i)
+    key[i] = __builtin_amdgcn_readfirstlane(i < seed_words ? seeds[(size_t)p * seed_words + i] : 0u);
 }
 
 SDA_DEV uint32_t draw(uint32_t w, const RngKey& rk, uint64_t retry_purpose, uint64_t owner,
@@ -124,6 +126,30 @@ __global__ void k_chacha_seeds(int P, int seed_words, RngKeyArg rng, uint64_t ow
 }
 
 // ------------------------------------------------------------- additive ----
+// 16 exact-uniform draws in [0, m) from one ChaCha block: the common path is a
+// Barrett reduction per word; rejected words (probability < m / 2^32 each) are
+// re-drawn from a private retry stream in a rarely taken, lane-divergent branch.
+SDA_DEV void draw16(uint32_t (&w)[16], const RngKey& rk, uint64_t purpose, uint64_t retry,
+                    uint64_t owner, uint64_t block, uint64_t idx0, uint64_t idx_stride,
+                    const ModParams& mp) {
+  rng_block(w, rk, stream_id(purpose, owner), block);
+  uint32_t rej = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    rej |= ((uint64_t)w[i] >= mp.zone32 ? 1u : 0u) << i;
+    w[i] = mod32(w[i], mp);
+  }
+  if (rej) {
+    for (int i = 0; i < 16; ++i)
+      if ((rej >> i) & 1)
+        w[i] = uniform_fixup(rk, retry, owner, idx0 + (uint64_t)i * idx_stride, mp.m,
+                             (uint32_t)mp.zone32);
+  }
+}
+
+// Per-clerk tile byte counts: wave partial sums in LDS, one barrier at the end.
+constexpr int kMaxCountSlots = 256;
+
 template <typename VT, int MASK>
 __global__ void __launch_bounds__(kBlock)
     k_share_additive(int P, int D, int n, ModParams mp, const int32_t* __restrict__ secrets,
@@ -131,72 +157,78 @@ __global__ void __launch_bounds__(kBlock)
                      uint32_t* __restrict__ cnt, uint32_t* __restrict__ mask_out,
                      uint32_t* __restrict__ mask_cnt, const uint32_t* __restrict__ seeds,
                      int seed_words, uint32_t* err) {
-  __shared__ uint32_t scratch[kWaves];
+  __shared__ uint32_t partial[kMaxCountSlots + 1][kWaves];
   const int t = blockIdx.x, p = blockIdx.y, T = gridDim.x;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int e0 = t * kTileValues + tid * 16;
   const int valid = max(0, min(16, D - e0));
   const uint64_t owner = owner_base + (uint64_t)p;
-  const uint64_t gthread = (uint64_t)t * kBlock + tid;
+  const uint64_t gidx = (uint64_t)e0 / 16;  // 16-element group index = ChaCha block id
   const RngKey rk = to_key(rng);
   const uint32_t m = mp.m;
   const bool vec_ok = (D % 16) == 0;
 
-  uint32_t x[16];
-  load16_secrets(x, secrets + (size_t)p * D + e0, valid, vec_ok, mp);
+  // `last` starts as the (masked) secret and becomes secret - sum(random shares)
+  uint32_t last[16];
+  load16_secrets(last, secrets + (size_t)p * D + e0, valid, vec_ok, mp);
 
   if constexpr (MASK == kMaskFull) {
-    uint32_t w[16], mk[16];
-    rng_block(w, rk, stream_id(kPurposeMaskFull, owner), gthread);
+    uint32_t w[16];
+    draw16(w, rk, kPurposeMaskFull, kPurposeMaskRetry, owner, gidx, (uint64_t)e0, 1, mp);
     uint32_t bytes = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      mk[i] = draw(w[i], rk, kPurposeMaskRetry, owner, (uint64_t)(e0 + i), mp);
-      x[i] = add_mod(x[i], mk[i], m);
-      bytes += i < valid ? vlen(mk[i]) : 0u;
+      last[i] = add_mod(last[i], w[i], m);
+      bytes += i < valid ? vlen(w[i]) : 0u;
     }
-    store16<uint32_t>(mask_out + (size_t)p * D + e0, mk, valid, vec_ok);
-    uint32_t tot = block_sum(bytes, scratch);
-    if (tid == 0) mask_cnt[(size_t)p * T + t] = tot;
+    store16<uint32_t>(mask_out + (size_t)p * D + e0, w, valid, vec_ok);
+    bytes = wave_sum(bytes);
+    if (lane == 0) partial[kMaxCountSlots][wave] = bytes;
   } else if constexpr (MASK == kMaskChaCha) {
     uint32_t key[8], mk[16];
     load_seed_key(key, seeds, p, seed_words);
     chacha_mask16(mk, key, (uint64_t)e0, mp, err);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] = add_mod(x[i], mk[i], m);
+    for (int i = 0; i < 16; ++i) last[i] = add_mod(last[i], mk[i], m);
   }
 
-  uint32_t sum[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) sum[i] = 0;
   const int w_draws = n - 1;
   for (int c = 0; c < w_draws; ++c) {
-    uint32_t w[16], r[16];
-    rng_block(w, rk, stream_id(kPurposeShares, owner), gthread * (uint64_t)w_draws + c);
+    uint32_t w[16];
+    draw16(w, rk, kPurposeShares, kPurposeSharesRetry, owner, gidx * (uint64_t)w_draws + c,
+           (uint64_t)e0 * (uint64_t)w_draws + c, (uint64_t)w_draws, mp);
     uint32_t bytes = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      r[i] = draw(w[i], rk, kPurposeSharesRetry, owner,
-                  (uint64_t)(e0 + i) * (uint64_t)w_draws + c, mp);
-      sum[i] = add_mod(sum[i], r[i], m);
-      bytes += i < valid ? vlen(r[i]) : 0u;
+      last[i] = sub_mod(last[i], w[i], m);
+      bytes += i < valid ? vlen(w[i]) : 0u;
     }
-    store16<VT>(shares + ((size_t)c * P + p) * D + e0, r, valid, vec_ok);
-    uint32_t tot = block_sum(bytes, scratch);
-    if (tid == 0) cnt[((size_t)c * P + p) * T + t] = tot;
+    store16<VT>(shares + ((size_t)c * P + p) * D + e0, w, valid, vec_ok);
+    bytes = wave_sum(bytes);
+    if (lane == 0) partial[c][wave] = bytes;
   }
   {
-    uint32_t r[16];
     uint32_t bytes = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      r[i] = sub_mod(x[i], sum[i], m);
-      bytes += i < valid ? vlen(r[i]) : 0u;
+    for (int i = 0; i < 16; ++i) bytes += i < valid ? vlen(last[i]) : 0u;
+    store16<VT>(shares + ((size_t)(n - 1) * P + p) * D + e0, last, valid, vec_ok);
+    bytes = wave_sum(bytes);
+    if (lane == 0) partial[n - 1][wave] = bytes;
+  }
+  __syncthreads();
+  for (int c = tid; c < n; c += kBlock) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += partial[c][w];
+    cnt[((size_t)c * P + p) * T + t] = s;
+  }
+  if constexpr (MASK == kMaskFull) {
+    if (tid == 0) {
+      uint32_t s = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) s += partial[kMaxCountSlots][w];
+      mask_cnt[(size_t)p * T + t] = s;
     }
-    const int c = n - 1;
-    store16<VT>(shares + ((size_t)c * P + p) * D + e0, r, valid, vec_ok);
-    uint32_t tot = block_sum(bytes, scratch);
-    if (tid == 0) cnt[((size_t)c * P + p) * T + t] = tot;
   }
 }
 
@@ -338,25 +370,32 @@ __global__ void __launch_bounds__(kBlock) k_count(int L, const VT* __restrict__ 
 }
 
 // ---------------------------------------------------- ChaCha mask (recipient)
+// out[e] = sum_p mask_p[e] mod m; each lane expands 8 elements (one ChaCha block)
+// of every participant's stream.
 __global__ void __launch_bounds__(kBlock)
     k_chacha_mask_sum(int P, int D, ModParams mp, int seed_words,
                       const uint32_t* __restrict__ seeds, uint32_t* __restrict__ out,
                       uint32_t* err) {
-  const int e0 = (blockIdx.x * kBlock + threadIdx.x) * 16;
+  const int e0 = (blockIdx.x * kBlock + threadIdx.x) * 8;
   if (e0 >= D) return;
-  uint64_t acc[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0;
+  uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  bool rej = false;
   for (int p = 0; p < P; ++p) {
-    uint32_t key[8], mk[16];
+    uint32_t key[8];
     load_seed_key(key, seeds, p, seed_words);
-    chacha_mask16(mk, key, (uint64_t)e0, mp, err);
+    uint32_t w[16];
+    chacharng_block(w, key, (uint64_t)e0 / 8);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] += mk[i];
+    for (int i = 0; i < 8; ++i) {
+      const uint64_t v = ((uint64_t)w[2 * i] << 32) | w[2 * i + 1];
+      rej |= v >= mp.zone64;
+      acc[i] = add_mod(acc[i], mod64(v, mp), mp.m);
+    }
   }
+  if (rej) atomicOr(err, kErrChaChaReject);
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (e0 + i < D) out[e0 + i] = mod64(acc[i], mp);
+  for (int i = 0; i < 8; ++i)
+    if (e0 + i < D) out[e0 + i] = acc[i];
 }
 
 }  // namespace
@@ -366,6 +405,7 @@ void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, con
                            void* shares, uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt,
                            uint32_t* seeds, uint32_t* err, hipStream_t s) {
   if (P <= 0 || D <= 0) return;
+  if (n < 2 || n > kMaxCountSlots) return;  // validated on the Python side
   ModParams mp = make_mod_params(m);
   if (mask_mode == kMaskChaCha)
     hipLaunchKernelGGL(k_chacha_seeds, dim3((P + 63) / 64), dim3(64), 0, s, P, seed_words, rng,
@@ -431,7 +471,7 @@ void launch_chacha_mask_sum(int P, int D, uint32_t m, int seed_words, const uint
                             uint32_t* out, uint32_t* err, hipStream_t s) {
   if (D <= 0) return;
   ModParams mp = make_mod_params(m);
-  int threads = (D + 15) / 16;
+  int threads = (D + 7) / 8;
   hipLaunchKernelGGL(k_chacha_mask_sum, dim3((threads + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
                      P, D, mp, seed_words, seeds, out, err);
 }

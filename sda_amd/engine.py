@@ -28,7 +28,7 @@ import torch
 from ._native import native
 from .models.schemes import Additive, AggregationSpec, ChaChaMask, FullMask, PackedShamir
 from .ops import gpu as G
-from .ops.sealed import Arena, open_, seal
+from .ops.sealed import Arena, open_, open_data, open_setup, seal, seal_data, seal_setup
 
 
 class AggregationError(RuntimeError):
@@ -99,124 +99,152 @@ class DeviceAggregator:
             marks.append((name, ev))
 
     # ---------------------------------------------------------- the round ----
-    def participate(self, secrets: torch.Tensor, rng_key: bytes, owner_base: int, err):
-        """Participant side for a wave of participants -> (clerk arena, mask arena)."""
+    def _share(self, secrets, rng_key, owner_base, err):
+        """Mask + share (+ byte counts): shares [n][P][B], cnt, mask values/seeds."""
         spec, n, m = self.spec, self.n, self.m
         P, D = secrets.shape
         B = spec.batches
-        T = G.tiles(B)
         dev = self.device
         shares = torch.empty(n, P, B, dtype=self.vdtype, device=dev)
-        cnt = torch.empty(n * P * T, dtype=torch.int32, device=dev)
-        mask_mode = G.MASK_NONE
-        mask_out = mask_cnt = seeds = None
-        seed_words = 0
+        cnt = torch.empty(n * P * G.tiles(B), dtype=torch.int32, device=dev)
+        mask_mode, mask_vals, mask_cnt, seed_words = G.MASK_NONE, None, None, 0
         if isinstance(spec.masking, FullMask):
             mask_mode = G.MASK_FULL
-            mask_out = torch.empty(P, D, dtype=torch.int32, device=dev)
+            mask_vals = torch.empty(P, D, dtype=torch.int32, device=dev)
             mask_cnt = torch.empty(P * G.tiles(D), dtype=torch.int32, device=dev)
         elif isinstance(spec.masking, ChaChaMask):
             mask_mode = G.MASK_CHACHA
             seed_words = spec.masking.seed_words
-            seeds = torch.empty(P, seed_words, dtype=torch.int32, device=dev)
+            mask_vals = torch.empty(P, seed_words, dtype=torch.int32, device=dev)
         if self._pss is None:
             G.share_additive(secrets, n, m, shares, cnt, mask_mode, rng_key, owner_base,
-                             mask_out=mask_out, mask_cnt=mask_cnt, seeds=seeds,
+                             mask_out=mask_vals if mask_mode == G.MASK_FULL else None,
+                             mask_cnt=mask_cnt,
+                             seeds=mask_vals if mask_mode == G.MASK_CHACHA else None,
                              seed_words=seed_words, err=err)
         else:
             ps = spec.sharing
             G.share_pss(secrets, n, ps.secret_count, ps.privacy_threshold_, m,
                         self._share_matrix, shares, cnt, mask_mode, rng_key, owner_base,
-                        mask_out=mask_out, seeds=seeds, seed_words=seed_words, err=err)
-            mask_cnt = None  # recounted by seal()
-        # clerk-major messages: j = c * P + p
-        key_idx = torch.arange(n, dtype=torch.int32, device=dev).repeat_interleave(P)
-        clerk_arena = seal(shares.view(n * P, B), key_idx, self.keys.pks, rng_key,
-                           owner_base * 64, err, m, cnt=cnt)
-        mask_arena = None
-        rkey = self._key_idx([n] * P)
-        if mask_mode == G.MASK_FULL:
-            mask_arena = seal(mask_out, rkey, self.keys.pks, rng_key, owner_base * 64 + n * P,
-                              err, m, cnt=mask_cnt)
-        elif mask_mode == G.MASK_CHACHA:
-            mask_arena = seal(seeds, rkey, self.keys.pks, rng_key, owner_base * 64 + (n + 1) * P,
-                              err, 0)
-        return clerk_arena, mask_arena
+                        mask_out=mask_vals if mask_mode == G.MASK_FULL else None,
+                        seeds=mask_vals if mask_mode == G.MASK_CHACHA else None,
+                        seed_words=seed_words, err=err)
+            mask_cnt = None  # PSS batches do not align with mask tiles: recounted
+        return shares, cnt, mask_vals, mask_cnt
 
-    def clerk(self, clerk_arena: Arena, P: int, rng_key: bytes, owner_base: int, err,
-              clerks: Sequence[int] | None = None) -> tuple[Arena, list]:
-        """All clerks: open their P boxes, combine, seal the sums for the recipient."""
-        n, m, B = self.n, self.m, self.spec.batches
-        dev = self.device
-        clerks = list(range(n)) if clerks is None else list(clerks)
-        # jobs of the participating clerks (contiguous per clerk)
-        if clerks == list(range(n)):
-            arena = clerk_arena
-        else:  # clerk dropout: only the live clerks' jobs are opened
-            parts = [clerk_arena.slice(c * P, P) for c in clerks]
-            arena = Arena(len(clerks) * P, B, m, clerk_arena.stride, clerk_arena.K,
-                          torch.cat([a.ct for a in parts]), torch.cat([a.pt_len for a in parts]))
-        key_idx = torch.tensor(clerks, dtype=torch.int32, device=dev).repeat_interleave(P)
-        vals = open_(arena, key_idx, self.keys.sks, self.keys.pks, err, out_dtype=self.vdtype)
-        combined = torch.empty(len(clerks), B, dtype=torch.int32, device=dev)
-        G.colsum(vals.view(len(clerks), P, B), m, combined)
-        res_vals = combined if self.vdtype == torch.int32 else combined.to(self.vdtype)
-        rkey = self._key_idx([n] * len(clerks))
-        res_arena = seal(res_vals, rkey, self.keys.pks, rng_key, owner_base, err, m)
-        return res_arena, clerks
-
-    def reveal(self, res_arena: Arena, clerks: list, mask_arena: Arena | None, P: int, err):
-        spec, n, m, D, B = self.spec, self.n, self.m, self.spec.dimension, self.spec.batches
-        dev = self.device
-        rk = self._key_idx([n] * res_arena.M)
-        ys = open_(res_arena, rk, self.keys.sks, self.keys.pks, err, out_dtype=torch.int32)
-        masked = torch.empty(D, dtype=torch.int32, device=dev)
-        if self._pss is None:
-            if len(clerks) != n:
-                raise AggregationError("additive sharing needs every clerk's result")
-            G.colsum(ys.view(1, n, B), m, masked)
-        else:
-            if len(clerks) < spec.sharing.reconstruction_threshold():
-                raise AggregationError("Not enough shares to reconstruct")
-            lag = torch.tensor(self._pss.lagrange_matrix(clerks), dtype=torch.int64).to(
-                torch.int32).to(dev)
-            G.pss_reconstruct(ys, lag, spec.sharing.secret_count, D, m, masked)
-        if mask_arena is None:
-            return masked
-        mask_sum = torch.empty(D, dtype=torch.int32, device=dev)
-        rkey = self._key_idx([n] * mask_arena.M)
-        if isinstance(spec.masking, FullMask):
-            masks = open_(mask_arena, rkey, self.keys.sks, self.keys.pks, err,
-                          out_dtype=torch.int32)
-            G.colsum(masks.view(1, P, D), m, mask_sum)
-        else:
-            seeds = open_(mask_arena, rkey, self.keys.sks, self.keys.pks, err,
-                          out_dtype=torch.int32)
-            G.chacha_mask_sum(seeds, D, m, mask_sum, err)
-        out = torch.empty(D, dtype=torch.int32, device=dev)
-        G.sub_mod(masked, mask_sum, m, out)
-        return out
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
 
     def run_round(self, secrets: torch.Tensor, clerks: Sequence[int] | None = None,
                   check: bool = True) -> RoundResult:
-        """One full round for participant vectors `secrets` [P][D] (int32, on device)."""
-        if secrets.dim() != 2 or secrets.shape[1] != self.spec.dimension:
+        """One full round for participant vectors `secrets` [P][D] (int32, on device).
+
+        Stream schedule: every X25519 / key-derivation kernel (participants'
+        ephemeral keys, clerks' and recipient's key agreement) runs on a side
+        stream concurrently with the bandwidth-bound share/encode/MAC kernels of
+        the main stream; the main stream waits on events only where it consumes
+        derived keys.
+        """
+        spec, n, m = self.spec, self.n, self.m
+        if secrets.dim() != 2 or secrets.shape[1] != spec.dimension:
             raise ValueError("secrets must be [P][dimension]")
         if secrets.dtype != torch.int32 or secrets.device.type != "cuda":
             raise ValueError("secrets must be an int32 GPU tensor")
         secrets = secrets.contiguous()
-        P = secrets.shape[0]
+        P, D = secrets.shape
+        B = spec.batches
+        live = list(range(n)) if clerks is None else sorted(set(int(c) for c in clerks))
+        if self._pss is None and len(live) != n:
+            raise AggregationError("additive sharing needs every clerk's result")
+        if self._pss is not None and len(live) < spec.sharing.reconstruction_threshold():
+            raise AggregationError("Not enough shares to reconstruct")
+        dev = self.device
         rng_key = native().crypto.random_bytes(32)
         self._round += 1
-        err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
         marks: list = []
         self._mark(marks, "start")
-        clerk_arena, mask_arena = self.participate(secrets, rng_key, 0, err)
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream()
+        pks, sks = self.keys.pks, self.keys.sks
+
+        # ---- arenas (participants -> clerks, participants -> recipient, clerks -> recipient)
+        clerk_arena = Arena.empty(n * P, B, m, dev)
+        mask_arena = None
+        if isinstance(spec.masking, FullMask):
+            mask_arena = Arena.empty(P, D, m, dev)
+        elif isinstance(spec.masking, ChaChaMask):
+            mask_arena = Arena.empty(P, spec.masking.seed_words, 0, dev)
+        res_arena = Arena.empty(len(live), B, m, dev)
+        kidx_clerk = torch.arange(n, dtype=torch.int32, device=dev).repeat_interleave(P)
+        kidx_rcpt_p = torch.full((P,), n, dtype=torch.int32, device=dev)
+        kidx_rcpt_c = torch.full((len(live),), n, dtype=torch.int32, device=dev)
+
+        # ---- side stream: all key agreement (data independent)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            ks_clerk = seal_setup(clerk_arena, kidx_clerk, pks, rng_key, 0, err)
+            ks_mask = (seal_setup(mask_arena, kidx_rcpt_p, pks, rng_key, n * P, err)
+                       if mask_arena is not None else None)
+            ks_res = seal_setup(res_arena, kidx_rcpt_c, pks, rng_key, (n + 1) * P, err)
+            ev_sealkeys = torch.cuda.Event()
+            ev_sealkeys.record(side)
+            ko_clerk = [open_setup(clerk_arena.slice(c * P, P), kidx_clerk[c * P:(c + 1) * P],
+                                   sks, pks, err) for c in live] if len(live) != n else \
+                [open_setup(clerk_arena, kidx_clerk, sks, pks, err)]
+            ko_res = open_setup(res_arena, kidx_rcpt_c, sks, pks, err)
+            ko_mask = (open_setup(mask_arena, kidx_rcpt_p, sks, pks, err)
+                       if mask_arena is not None else None)
+            ev_openkeys = torch.cuda.Event()
+            ev_openkeys.record(side)
+        for t in [ks_clerk, ks_mask, ks_res, ko_res, ko_mask] + ko_clerk:
+            if t is not None:
+                t.record_stream(main)
+
+        # ---- participants: mask + share, then encrypt (waits for the seal keys)
+        shares, cnt, mask_vals, mask_cnt = self._share(secrets, rng_key, 0, err)
+        main.wait_event(ev_sealkeys)
+        seal_data(clerk_arena, ks_clerk, shares.view(n * P, B), err, cnt)
+        if mask_arena is not None:
+            seal_data(mask_arena, ks_mask, mask_vals, err, mask_cnt)
         self._mark(marks, "participate")
-        res_arena, used = self.clerk(clerk_arena, P, rng_key, 1 << 48, err, clerks)
+
+        # ---- clerks: verify + decrypt + decode their P boxes, combine, reseal
+        main.wait_event(ev_openkeys)
+        if len(live) == n:
+            vals = open_data(clerk_arena, ko_clerk[0], err, out_dtype=self.vdtype)
+        else:
+            vals = torch.empty(len(live), P, B, dtype=self.vdtype, device=dev)
+            for i, c in enumerate(live):
+                open_data(clerk_arena.slice(c * P, P), ko_clerk[i], err, out=vals[i])
+        combined = torch.empty(len(live), B, dtype=torch.int32, device=dev)
+        G.colsum(vals.view(len(live), P, B), m, combined)
+        res_vals = combined if self.vdtype == torch.int32 else combined.to(self.vdtype)
+        seal_data(res_arena, ks_res, res_vals, err)
         self._mark(marks, "clerk")
-        out = self.reveal(res_arena, used, mask_arena, P, err)
+
+        # ---- recipient: open results, reconstruct, unmask
+        ys = open_data(res_arena, ko_res, err, out_dtype=torch.int32)
+        masked = torch.empty(D, dtype=torch.int32, device=dev)
+        if self._pss is None:
+            G.colsum(ys.view(1, n, B), m, masked)
+        else:
+            lag = self._lagrange(live)
+            G.pss_reconstruct(ys, lag, spec.sharing.secret_count, D, m, masked)
+        out = masked
+        if mask_arena is not None:
+            mask_sum = torch.empty(D, dtype=torch.int32, device=dev)
+            mvals = open_data(mask_arena, ko_mask, err, out_dtype=torch.int32)
+            if isinstance(spec.masking, FullMask):
+                G.colsum(mvals.view(1, P, D), m, mask_sum)
+            else:
+                G.chacha_mask_sum(mvals, D, m, mask_sum, err)
+            out = torch.empty(D, dtype=torch.int32, device=dev)
+            G.sub_mod(masked, mask_sum, m, out)
         self._mark(marks, "reveal")
+
         stage_ms = {}
         if check or self.time_stages:
             e = int(err.item())
@@ -224,7 +252,17 @@ class DeviceAggregator:
                 raise AggregationError(f"device error word 0x{e:x} ({describe_error(e)})")
             for (a, ea), (b, eb) in zip(marks, marks[1:]):
                 stage_ms[b] = ea.elapsed_time(eb)
-        return RoundResult(out, used, stage_ms)
+        return RoundResult(out, live, stage_ms)
+
+    def _lagrange(self, live):
+        key = tuple(live)
+        cache = getattr(self, "_lag_cache", None)
+        if cache is None:
+            cache = self._lag_cache = {}
+        if key not in cache:
+            cache[key] = torch.tensor(self._pss.lagrange_matrix(list(live)), dtype=torch.int64).to(
+                torch.int32).to(self.device)
+        return cache[key]
 
 
 def describe_error(e: int) -> str:

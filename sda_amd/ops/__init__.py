@@ -1,3 +1,3 @@
 """gfx950 HIP kernel ops (see csrc/kernels)."""
 from . import gpu  # noqa: F401
-from .sealed import Arena, seal, open_  # noqa: F401
+from .sealed import Arena, seal, open_, seal_setup, seal_data, open_setup, open_data  # noqa: F401

@@ -81,14 +81,25 @@ class Arena:
                      self.pt_len[first:first + count])
 
 
-def seal(values: torch.Tensor, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: bytes,
-         owner_base: int, err: torch.Tensor, modulus: int, cnt: torch.Tensor | None = None,
-         arena: Arena | None = None) -> Arena:
-    """Seal each row of `values` [M][L] for public key pks[key_idx[row]]."""
+def seal_setup(arena: Arena, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: bytes,
+               owner_base: int, err: torch.Tensor) -> torch.Tensor:
+    """Ephemeral keypairs + X25519 + nonce/subkey derivation for every slot.
+
+    Independent of the message contents, so the engine runs it on a side stream
+    concurrently with share generation. Writes epk into each slot header.
+    """
+    keys = torch.empty(arena.M * G.MSGKEY_BYTES, dtype=torch.uint8, device=arena.ct.device)
+    G.seal_setup(arena.M, rng_key, owner_base, key_idx, pks, arena.ct, arena.stride, keys, err)
+    return keys
+
+
+def seal_data(arena: Arena, keys: torch.Tensor, values: torch.Tensor, err: torch.Tensor,
+              cnt: torch.Tensor | None = None) -> Arena:
+    """Varint-encode + encrypt + MAC the rows of `values` [M][L] into `arena`."""
     M, L = values.shape
+    if M != arena.M or L != arena.L:
+        raise ValueError("values do not match the arena shape")
     dev = values.device
-    if arena is None:
-        arena = Arena.empty(M, L, modulus, dev)
     T = G.tiles(L)
     if cnt is None:
         cnt = torch.empty(M, T, dtype=torch.int32, device=dev)
@@ -96,8 +107,6 @@ def seal(values: torch.Tensor, key_idx: torch.Tensor, pks: torch.Tensor, rng_key
     else:
         cnt = cnt.view(M, T)
     G.segscan(cnt, arena.pt_len)  # cnt becomes the tile byte offsets
-    keys = torch.empty(M * G.MSGKEY_BYTES, dtype=torch.uint8, device=dev)
-    G.seal_setup(M, rng_key, owner_base, key_idx, pks, arena.ct, arena.stride, keys, err)
     G.encode_encrypt(values, cnt, keys, arena.ct, arena.stride)
     partials = torch.empty(M * arena.K * 8, dtype=torch.int32, device=dev)
     G.mac_chunks(M, arena.K, keys, arena.ct, arena.stride, arena.pt_len, partials, decrypt=False)
@@ -106,17 +115,33 @@ def seal(values: torch.Tensor, key_idx: torch.Tensor, pks: torch.Tensor, rng_key
     return arena
 
 
-def open_(arena: Arena, key_idx: torch.Tensor, sks: torch.Tensor, pks: torch.Tensor,
-          err: torch.Tensor, out_dtype: torch.dtype | None = None,
-          out: torch.Tensor | None = None) -> torch.Tensor:
+def seal(values: torch.Tensor, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: bytes,
+         owner_base: int, err: torch.Tensor, modulus: int, cnt: torch.Tensor | None = None,
+         arena: Arena | None = None) -> Arena:
+    """Seal each row of `values` [M][L] for public key pks[key_idx[row]]."""
+    M, L = values.shape
+    if arena is None:
+        arena = Arena.empty(M, L, modulus, values.device)
+    keys = seal_setup(arena, key_idx, pks, rng_key, owner_base, err)
+    return seal_data(arena, keys, values, err, cnt)
+
+
+def open_setup(arena: Arena, key_idx: torch.Tensor, sks: torch.Tensor, pks: torch.Tensor,
+               err: torch.Tensor) -> torch.Tensor:
+    """X25519(sk, epk) + derivations for every slot (needs only the headers)."""
+    keys = torch.empty(arena.M * G.MSGKEY_BYTES, dtype=torch.uint8, device=arena.ct.device)
+    G.open_setup(arena.M, key_idx, sks, pks, arena.ct, arena.stride, keys, err)
+    return keys
+
+
+def open_data(arena: Arena, keys: torch.Tensor, err: torch.Tensor,
+              out_dtype: torch.dtype | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """Verify + decrypt (in place) + decode every message; returns [M][L] values.
 
     Destroys the ciphertext (it is replaced by plaintext).
     """
     M, L, K = arena.M, arena.L, arena.K
     dev = arena.ct.device
-    keys = torch.empty(M * G.MSGKEY_BYTES, dtype=torch.uint8, device=dev)
-    G.open_setup(M, key_idx, sks, pks, arena.ct, arena.stride, keys, err)
     partials = torch.empty(M * K * 8, dtype=torch.int32, device=dev)
     term = torch.empty(M, K, dtype=torch.int32, device=dev)
     G.mac_chunks(M, K, keys, arena.ct, arena.stride, arena.pt_len, partials, decrypt=True,
@@ -130,3 +155,10 @@ def open_(arena: Arena, key_idx: torch.Tensor, sks: torch.Tensor, pks: torch.Ten
         out = torch.empty(M, L, dtype=out_dtype or G.value_dtype(arena.modulus), device=dev)
     G.decode(M, K, L, arena.modulus, arena.ct, arena.stride, arena.pt_len, term, out, err)
     return out
+
+
+def open_(arena: Arena, key_idx: torch.Tensor, sks: torch.Tensor, pks: torch.Tensor,
+          err: torch.Tensor, out_dtype: torch.dtype | None = None,
+          out: torch.Tensor | None = None) -> torch.Tensor:
+    keys = open_setup(arena, key_idx, sks, pks, err)
+    return open_data(arena, keys, err, out_dtype, out)
