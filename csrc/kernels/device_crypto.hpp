@@ -303,161 +303,181 @@ SDA_DEV void p130_finish(uint32_t (&tag)[4], P130 h, const uint32_t (&s)[4]) {
 }
 
 // -------------------------------------------------------- GF(2^255 - 19) ----
-struct Fe {
-  uint32_t v[8];
+// ---- radix 2^25.5 representation (10 limbs, 26/25 bits alternating) -------
+// Products accumulate into 10 independent 64-bit column sums (no carry chain
+// inside the product), which gives the single-wave X25519 ladders the ILP the
+// serial radix-2^32 schoolbook lacks. Limb i sits at bit ceil(25.5 i); a product
+// of two odd limbs is doubled, and columns >= 10 wrap with a factor 19.
+struct Fe10 {
+  uint32_t v[10];
 };
-SDA_DEV Fe fe_set(uint32_t x) { return Fe{{x, 0, 0, 0, 0, 0, 0, 0}}; }
+SDA_DEV Fe10 fe10_set(uint32_t x) { return Fe10{{x, 0, 0, 0, 0, 0, 0, 0, 0, 0}}; }
 
-SDA_DEV Fe fe_add(const Fe& a, const Fe& b) {
-  Fe r;
-  uint64_t c = 0;
+SDA_DEV Fe10 fe10_carry64(uint64_t (&h)[10]) {
+  uint64_t c;
+  c = h[0] >> 26; h[1] += c; h[0] &= 0x3ffffff;
+  c = h[1] >> 25; h[2] += c; h[1] &= 0x1ffffff;
+  c = h[2] >> 26; h[3] += c; h[2] &= 0x3ffffff;
+  c = h[3] >> 25; h[4] += c; h[3] &= 0x1ffffff;
+  c = h[4] >> 26; h[5] += c; h[4] &= 0x3ffffff;
+  c = h[5] >> 25; h[6] += c; h[5] &= 0x1ffffff;
+  c = h[6] >> 26; h[7] += c; h[6] &= 0x3ffffff;
+  c = h[7] >> 25; h[8] += c; h[7] &= 0x1ffffff;
+  c = h[8] >> 26; h[9] += c; h[8] &= 0x3ffffff;
+  c = h[9] >> 25; h[0] += c * 19; h[9] &= 0x1ffffff;
+  c = h[0] >> 26; h[1] += c; h[0] &= 0x3ffffff;
+  Fe10 r;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { c += (uint64_t)a.v[i] + b.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-  c *= 38;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-  r.v[0] += (uint32_t)(c * 38);
+  for (int i = 0; i < 10; ++i) r.v[i] = (uint32_t)h[i];
   return r;
 }
-SDA_DEV Fe fe_sub(const Fe& a, const Fe& b) {
-  Fe r;
-  int64_t c = 0;
+SDA_DEV Fe10 fe10_carry(const Fe10& a) {
+  uint64_t h[10];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { c += (int64_t)a.v[i] - (int64_t)b.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-  c *= 38;  // borrow -> subtract 38 (2^256 == 38)
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-  r.v[0] -= (uint32_t)((-c) * 38);
-  return r;
+  for (int i = 0; i < 10; ++i) h[i] = a.v[i];
+  return fe10_carry64(h);
 }
-SDA_DEV Fe fe_reduce512(const uint32_t (&t)[16]) {
-  Fe r;
-  uint64_t c = 0;
+SDA_DEV Fe10 fe10_add(const Fe10& a, const Fe10& b) {
+  Fe10 r;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    c += (uint64_t)t[i] + (uint64_t)t[i + 8] * 38;
-    r.v[i] = (uint32_t)c;
-    c >>= 32;
+  for (int i = 0; i < 10; ++i) r.v[i] = a.v[i] + b.v[i];
+  return fe10_carry(r);
+}
+// a - b + 2p, then carried (inputs carried: limbs <= 2^26 + small)
+SDA_DEV Fe10 fe10_sub(const Fe10& a, const Fe10& b) {
+  Fe10 r;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t two_p = (i == 0) ? 0x7ffffdau : ((i & 1) ? 0x3fffffeu : 0x7fffffeu);
+    r.v[i] = a.v[i] + two_p - b.v[i];
   }
-  c *= 38;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-  r.v[0] += (uint32_t)(c * 38);
-  return r;
+  return fe10_carry(r);
 }
-SDA_DEV Fe fe_mul(const Fe& a, const Fe& b) {
-  uint32_t t[16];
+SDA_DEV Fe10 fe10_mul(const Fe10& f, const Fe10& g) {
+  uint32_t g19[10], f2[10];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) t[i] = 0;
+  for (int i = 0; i < 10; ++i) {
+    g19[i] = 19u * g.v[i];
+    f2[i] = (i & 1) ? 2u * f.v[i] : f.v[i];
+  }
+  uint64_t h[10];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint64_t c = 0;
+  for (int k = 0; k < 10; ++k) h[k] = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      c += (uint64_t)a.v[i] * b.v[j] + t[i + j];
-      t[i + j] = (uint32_t)c;
-      c >>= 32;
+  for (int i = 0; i < 10; ++i) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const uint32_t fi = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      if (i + j < 10) h[i + j] += (uint64_t)fi * g.v[j];
+      else h[i + j - 10] += (uint64_t)fi * g19[j];
     }
-    t[i + 8] = (uint32_t)c;
   }
-  return fe_reduce512(t);
+  return fe10_carry64(h);
 }
-SDA_DEV Fe fe_sq(const Fe& a) {
-  // off-diagonal products once, doubled, plus the diagonal
-  uint32_t t[16];
+SDA_DEV Fe10 fe10_sq(const Fe10& f) {
+  uint32_t f19[10], f2[10];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) t[i] = 0;
+  for (int i = 0; i < 10; ++i) {
+    f19[i] = 19u * f.v[i];
+    f2[i] = 2u * f.v[i];
+  }
+  uint64_t h[10];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint64_t c = 0;
+  for (int k = 0; k < 10; ++k) h[k] = 0;
 #pragma unroll
-    for (int j = i + 1; j < 8; ++j) {
-      c += (uint64_t)a.v[i] * a.v[j] + t[i + j];
-      t[i + j] = (uint32_t)c;
-      c >>= 32;
+  for (int i = 0; i < 10; ++i) {
+#pragma unroll
+    for (int j = i; j < 10; ++j) {
+      // symmetric pair counted twice (i != j); odd*odd doubles once more
+      const bool odd2 = (i & 1) && (j & 1);
+      uint32_t a = (i == j) ? (odd2 ? f2[i] : f.v[i]) : (odd2 ? 2u * f2[i] : f2[i]);
+      if (i + j < 10) h[i + j] += (uint64_t)a * f.v[j];
+      else h[i + j - 10] += (uint64_t)a * f19[j];
     }
-    t[i + 8] = (uint32_t)c;
   }
-  uint32_t top = 0;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {  // double
-    uint32_t nt = t[i] >> 31;
-    t[i] = (t[i] << 1) | top;
-    top = nt;
-  }
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint64_t sq = (uint64_t)a.v[i] * a.v[i];
-    c += (uint64_t)t[2 * i] + (uint32_t)sq;
-    t[2 * i] = (uint32_t)c;
-    c >>= 32;
-    c += (uint64_t)t[2 * i + 1] + (uint32_t)(sq >> 32);
-    t[2 * i + 1] = (uint32_t)c;
-    c >>= 32;
-  }
-  return fe_reduce512(t);
+  return fe10_carry64(h);
 }
-SDA_DEV Fe fe_mul_small(const Fe& a, uint32_t s) {
-  Fe r;
-  uint64_t c = 0;
+SDA_DEV Fe10 fe10_mul121665(const Fe10& f) {
+  uint64_t h[10];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { c += (uint64_t)a.v[i] * s; r.v[i] = (uint32_t)c; c >>= 32; }
-  c *= 38;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-  r.v[0] += (uint32_t)(c * 38);
-  return r;
+  for (int i = 0; i < 10; ++i) h[i] = (uint64_t)f.v[i] * 121665u;
+  return fe10_carry64(h);
 }
-SDA_DEV Fe fe_sqn(Fe a, int n) {
-  for (int i = 0; i < n; ++i) a = fe_sq(a);
-  return a;
-}
-SDA_DEV Fe fe_invert(const Fe& z) {
-  Fe z2 = fe_sq(z);
-  Fe z8 = fe_sqn(z2, 2);
-  Fe z9 = fe_mul(z8, z);
-  Fe z11 = fe_mul(z9, z2);
-  Fe z22 = fe_sq(z11);
-  Fe z_5_0 = fe_mul(z22, z9);
-  Fe z_10_0 = fe_mul(fe_sqn(z_5_0, 5), z_5_0);
-  Fe z_20_0 = fe_mul(fe_sqn(z_10_0, 10), z_10_0);
-  Fe z_40_0 = fe_mul(fe_sqn(z_20_0, 20), z_20_0);
-  Fe z_50_0 = fe_mul(fe_sqn(z_40_0, 10), z_10_0);
-  Fe z_100_0 = fe_mul(fe_sqn(z_50_0, 50), z_50_0);
-  Fe z_200_0 = fe_mul(fe_sqn(z_100_0, 100), z_100_0);
-  Fe z_250_0 = fe_mul(fe_sqn(z_200_0, 50), z_50_0);
-  return fe_mul(fe_sqn(z_250_0, 5), z11);
-}
-// Fully reduce to [0, p).
-SDA_DEV Fe fe_canon(Fe r) {
+SDA_DEV void fe10_cswap(Fe10& a, Fe10& b, uint32_t swap) {
+  const uint32_t mask = 0u - swap;
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    uint32_t top = r.v[7] >> 31;
-    r.v[7] &= 0x7fffffffu;
-    uint64_t c = (uint64_t)top * 19;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-  }
-  // r < 2^255 + small; subtract p if r >= p  <=>  r + 19 >= 2^255
-  Fe t;
-  uint64_t c = 19;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { c += r.v[i]; t.v[i] = (uint32_t)c; c >>= 32; }
-  uint32_t ge = t.v[7] >> 31;
-  t.v[7] &= 0x7fffffffu;
-  uint32_t mask = 0u - ge;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = (r.v[i] & ~mask) | (t.v[i] & mask);
-  return r;
-}
-SDA_DEV void fe_cswap(Fe& a, Fe& b, uint32_t swap) {
-  uint32_t mask = 0u - swap;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint32_t t = mask & (a.v[i] ^ b.v[i]);
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t t = mask & (a.v[i] ^ b.v[i]);
     a.v[i] ^= t;
     b.v[i] ^= t;
+  }
+}
+SDA_DEV Fe10 fe10_sqn(Fe10 a, int n) {
+  for (int i = 0; i < n; ++i) a = fe10_sq(a);
+  return a;
+}
+SDA_DEV Fe10 fe10_invert(const Fe10& z) {
+  Fe10 z2 = fe10_sq(z);
+  Fe10 z9 = fe10_mul(fe10_sqn(z2, 2), z);
+  Fe10 z11 = fe10_mul(z9, z2);
+  Fe10 z_5_0 = fe10_mul(fe10_sq(z11), z9);
+  Fe10 z_10_0 = fe10_mul(fe10_sqn(z_5_0, 5), z_5_0);
+  Fe10 z_20_0 = fe10_mul(fe10_sqn(z_10_0, 10), z_10_0);
+  Fe10 z_40_0 = fe10_mul(fe10_sqn(z_20_0, 20), z_20_0);
+  Fe10 z_50_0 = fe10_mul(fe10_sqn(z_40_0, 10), z_10_0);
+  Fe10 z_100_0 = fe10_mul(fe10_sqn(z_50_0, 50), z_50_0);
+  Fe10 z_200_0 = fe10_mul(fe10_sqn(z_100_0, 100), z_100_0);
+  Fe10 z_250_0 = fe10_mul(fe10_sqn(z_200_0, 50), z_50_0);
+  return fe10_mul(fe10_sqn(z_250_0, 5), z11);
+}
+SDA_DEV Fe10 fe10_from_words(const uint32_t (&w)[8]) {
+  // bit offsets 0,26,51,77,102,128,153,179,204,230
+  const int pos[10] = {0, 26, 51, 77, 102, 128, 153, 179, 204, 230};
+  Fe10 r;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const int p = pos[i], wi = p >> 5, sh = p & 31;
+    const int width = (i & 1) ? 25 : 26;
+    uint64_t x = w[wi];
+    if (wi + 1 < 8) x |= (uint64_t)w[wi + 1] << 32;
+    r.v[i] = (uint32_t)(x >> sh) & ((1u << width) - 1);
+  }
+  r.v[9] &= 0x1ffffff;  // bit 255 ignored (limb 9 covers bits 230..254)
+  return r;
+}
+SDA_DEV void fe10_to_words(uint32_t (&w)[8], const Fe10& a) {
+  // fully reduce: carry, then subtract p if h >= p
+  uint64_t h[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h[i] = a.v[i];
+  Fe10 t = fe10_carry64(h);
+  t = fe10_carry(t);
+  // q = 1 iff t >= p: propagate (t + 19) carries to bit 255
+  uint32_t q = (19u * 1u + t.v[0]) >> 26;
+#pragma unroll
+  for (int i = 1; i < 10; ++i) q = (t.v[i] + q) >> ((i & 1) ? 25 : 26);
+  uint64_t hh[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) hh[i] = t.v[i];
+  hh[0] += 19u * q;
+  uint64_t c;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int width = (i & 1) ? 25 : 26;
+    c = hh[i] >> width;
+    hh[i + 1] += c;
+    hh[i] &= (1u << width) - 1;
+  }
+  hh[9] &= 0x1ffffff;
+  const int pos[10] = {0, 26, 51, 77, 102, 128, 153, 179, 204, 230};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const int p = pos[i], wi = p >> 5, sh = p & 31;
+    const uint64_t x = hh[i] << sh;
+    w[wi] |= (uint32_t)x;
+    if (wi + 1 < 8) w[wi + 1] |= (uint32_t)(x >> 32);
   }
 }
 
@@ -469,33 +489,28 @@ SDA_DEV void x25519(uint32_t (&out)[8], const uint32_t (&scalar)[8], const uint3
   k[0] &= 0xfffffff8u;
   k[7] &= 0x7fffffffu;
   k[7] |= 0x40000000u;
-  Fe x1;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) x1.v[i] = u[i];
-  x1.v[7] &= 0x7fffffffu;
-  Fe x2 = fe_set(1), z2 = fe_set(0), x3 = x1, z3 = fe_set(1);
+  const Fe10 x1 = fe10_from_words(u);
+  Fe10 x2 = fe10_set(1), z2 = fe10_set(0), x3 = x1, z3 = fe10_set(1);
   uint32_t swap = 0;
   for (int t = 254; t >= 0; --t) {
-    uint32_t kt = (k[t >> 5] >> (t & 31)) & 1;
+    const uint32_t kt = (k[t >> 5] >> (t & 31)) & 1;
     swap ^= kt;
-    fe_cswap(x2, x3, swap);
-    fe_cswap(z2, z3, swap);
+    fe10_cswap(x2, x3, swap);
+    fe10_cswap(z2, z3, swap);
     swap = kt;
-    Fe A = fe_add(x2, z2), AA = fe_sq(A);
-    Fe B = fe_sub(x2, z2), BB = fe_sq(B);
-    Fe E = fe_sub(AA, BB);
-    Fe C = fe_add(x3, z3), D = fe_sub(x3, z3);
-    Fe DA = fe_mul(D, A), CB = fe_mul(C, B);
-    x3 = fe_sq(fe_add(DA, CB));
-    z3 = fe_mul(x1, fe_sq(fe_sub(DA, CB)));
-    x2 = fe_mul(AA, BB);
-    z2 = fe_mul(E, fe_add(AA, fe_mul_small(E, 121665)));
+    const Fe10 A = fe10_add(x2, z2), B = fe10_sub(x2, z2);
+    const Fe10 C = fe10_add(x3, z3), D = fe10_sub(x3, z3);
+    const Fe10 AA = fe10_sq(A), BB = fe10_sq(B);
+    const Fe10 DA = fe10_mul(D, A), CB = fe10_mul(C, B);
+    const Fe10 E = fe10_sub(AA, BB);
+    x3 = fe10_sq(fe10_add(DA, CB));
+    z3 = fe10_mul(x1, fe10_sq(fe10_sub(DA, CB)));
+    x2 = fe10_mul(AA, BB);
+    z2 = fe10_mul(E, fe10_add(AA, fe10_mul121665(E)));
   }
-  fe_cswap(x2, x3, swap);
-  fe_cswap(z2, z3, swap);
-  Fe r = fe_canon(fe_mul(x2, fe_invert(z2)));
-#pragma unroll
-  for (int i = 0; i < 8; ++i) out[i] = r.v[i];
+  fe10_cswap(x2, x3, swap);
+  fe10_cswap(z2, z3, swap);
+  fe10_to_words(out, fe10_mul(x2, fe10_invert(z2)));
 }
 
 // ------------------------------------------------------------------ varint --

@@ -156,6 +156,21 @@ int main() {
     bytes(db2, bw, 6);
     CHECK(std::memcmp(b2, db2, 24) == 0, "blake2b");
   }
+  // 1b. device X25519 (radix 2^25.5 ladder) vs host
+  for (int it = 0; it < 32; ++it) {
+    uint8_t sc[32], pt[32], ho[32];
+    hc::os_random(sc, 32);
+    hc::os_random(pt, 32);
+    if (it == 0) { std::memset(pt, 0, 32); pt[0] = 9; }
+    if (it == 1) std::memset(pt, 0xff, 32);  // non-canonical u
+    hc::x25519(ho, sc, pt);
+    uint32_t sw[8], pw[8], dw[8];
+    words(sw, sc, 8); words(pw, pt, 8);
+    x25519(dw, sw, pw);
+    uint8_t db[32];
+    bytes(db, dw, 8);
+    CHECK(std::memcmp(ho, db, 32) == 0, "x25519 it=%d", it);
+  }
   // 2. message key derivation vs host crypto_box_seal
   uint8_t pk[32], sk[32], esk[32], epk[32];
   hc::box_keypair(pk, sk);

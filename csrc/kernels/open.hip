@@ -91,34 +91,71 @@ __global__ void __launch_bounds__(kBlock)
   uint32_t total;
   uint32_t local = block_excl_scan((uint32_t)__popcll(tmask), scratch, &total);  // syncs
   bool bad = false;
-  uint64_t acc = 0;
-  uint32_t shift = 0;
-  if (vmask) {
-    // carry-in: continuation bytes right before this lane's first valid byte
-    const int64_t s = p0 + lo;
-    int n = 0;
-    while (n < 10 && s - n - 1 >= 0 && (buf[16 + (s - n - 1) - (kC - 32)] & 0x80)) ++n;
-    bad |= n >= 10;
-    for (int u = 0; u < n && u < 9; ++u) {
-      acc |= (uint64_t)(buf[16 + (s - n + u) - (kC - 32)] & 0x7f) << shift;
-      shift += 7;
+  const int64_t img = 16 - (kC - 32);  // LDS index of message position 0
+  // The two bytes preceding this lane's range (previous lane's last word; lane 0
+  // of each wave reads them from the LDS image, which holds the chunk prefix).
+  uint32_t prev_word = __shfl_up(w[15], 1, 64);
+  if ((tid & 63) == 0) {
+    const int64_t q = p0 - 4;
+    prev_word = 0;
+    for (int u = 0; u < 4; ++u) {
+      const int64_t pos = q + u;
+      const uint32_t byte = (pos >= 0 && pos >= kC - 48) ? buf[img + pos] : 0u;
+      prev_word |= byte << (8 * u);
     }
   }
+  // Static pass over the 64 bytes, all in registers (the LDS image is only
+  // touched by the rare long-varint walk: lanes 64 B apart would all hit the
+  // same two LDS banks). A terminator at b closes a 1-, 2- or 3-byte varint
+  // depending on the continuation bits of bytes b-1, b-2; four bytes and more
+  // (|value| >= 2^20) take the LDS walk below.
+  uint32_t long_mask_lo = 0, long_mask_hi = 0;  // terminators needing the slow path
+  uint32_t b3 = (prev_word >> 8) & 0xffu, b2 = (prev_word >> 16) & 0xffu, b1 = prev_word >> 24;
 #pragma unroll
   for (int b = 0; b < 64; ++b) {
-    if ((vmask >> b) & 1) {
-      const uint32_t byte = (w[b >> 2] >> (8 * (b & 3))) & 0xffu;
-      if (shift < 64) acc |= (uint64_t)(byte & 0x7f) << shift;
-      shift += 7;
-      if (!(byte & 0x80)) {
-        bad |= shift > 70;
-        outb[local++] = (VT)canon_varint(acc, mp, bad);
-        acc = 0;
-        shift = 0;
+    const uint32_t byte = (w[b >> 2] >> (8 * (b & 3))) & 0xffu;
+    if ((tmask >> b) & 1) {
+      uint64_t z;
+      if (!(b1 & 0x80)) {
+        z = byte;
+      } else if (!(b2 & 0x80)) {
+        z = (b1 & 0x7f) | (byte << 7);
+      } else {
+        z = (b2 & 0x7f) | ((b1 & 0x7f) << 7) | (byte << 14);
+        if (b3 & 0x80) {
+          if (b < 32) long_mask_lo |= 1u << b; else long_mask_hi |= 1u << (b - 32);
+        }
       }
+      outb[local] = (VT)canon_varint(z, mp, bad);
+      ++local;
+    }
+    b3 = b2;
+    b2 = b1;
+    b1 = byte;
+  }
+  // rare slow path: rewrite the values of >= 3-byte varints
+  uint64_t lm = ((uint64_t)long_mask_hi << 32) | long_mask_lo;
+  if (lm) {
+    uint32_t rank0 = local - (uint32_t)__popcll(tmask);
+    while (lm) {
+      const int b = __builtin_ctzll(lm);
+      lm &= lm - 1;
+      const uint32_t r = rank0 + (uint32_t)__popcll(tmask & ((1ull << b) - 1));
+      const int64_t q = p0 + b;
+      int64_t s0 = q;
+      int n = 0;
+      while (n < 10 && s0 > 0 && (buf[img + s0 - 1] & 0x80)) { --s0; ++n; }
+      bad |= n >= 10;
+      uint64_t z = 0;
+      for (int64_t u = s0; u <= q; ++u) {
+        const uint32_t sh = 7u * (uint32_t)(u - s0);
+        if (sh < 64) z |= (uint64_t)(buf[img + u] & 0x7f) << sh;
+      }
+      outb[r] = (VT)canon_varint(z, mp, bad);
     }
   }
-  if (p0 + hi == (int64_t)N && hi > lo && shift != 0) bad = true;  // dangling continuation
+  // a message must end on a terminator
+  if (hi > lo && p0 + hi == (int64_t)N && (buf[img + N - 1] & 0x80)) bad = true;
   __syncthreads();
   const uint32_t base = elem_start[(size_t)j * K + k];
   VT* out = vals + (size_t)j * L;

@@ -165,6 +165,7 @@ __global__ void __launch_bounds__(kBlock)
                  uint32_t* __restrict__ term_cnt) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kChunkBytes];
   __shared__ uint32_t tree[5][kBlock];
+  __shared__ uint32_t rpow[8][5];
   __shared__ uint32_t scratch[kWaves];
   const int k = blockIdx.x, j = blockIdx.y, K = gridDim.x;
   const int tid = threadIdx.x;
@@ -203,8 +204,17 @@ __global__ void __launch_bounds__(kBlock)
     if (i >= fb) c = load_block(buf, i, kC, N);
     h = p130_mul(p130_add(h, c), r);
   }
-  P130 R = p130_mul(r, r);
-  R = p130_mul(R, R);  // r^4
+  // r^(4 * 2^l), l = 0..7, computed once per block (lane 0) into LDS
+  if (tid == 0) {
+    P130 R = p130_mul(r, r);
+    R = p130_mul(R, R);
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+#pragma unroll
+      for (int u = 0; u < 5; ++u) rpow[l][u] = R.v[u];
+      R = p130_mul(R, R);
+    }
+  }
 #pragma unroll
   for (int l = 0; l < 8; ++l) {
     const int s = 1 << l;
@@ -213,12 +223,14 @@ __global__ void __launch_bounds__(kBlock)
     for (int u = 0; u < 5; ++u) tree[u][tid] = h.v[u];
     __syncthreads();
     if ((tid & (2 * s - 1)) == 2 * s - 1) {
-      P130 left;
+      P130 left, R;
 #pragma unroll
-      for (int u = 0; u < 5; ++u) left.v[u] = tree[u][tid - s];
+      for (int u = 0; u < 5; ++u) {
+        left.v[u] = tree[u][tid - s];
+        R.v[u] = rpow[l][u];
+      }
       h = p130_carry(p130_add(p130_mul(left, R), h));
     }
-    R = p130_mul(R, R);
   }
   if (tid == kBlock - 1) {
 #pragma unroll
@@ -240,20 +252,25 @@ __global__ void __launch_bounds__(kBlock)
         q[u] = d;
       }
     }
-    // terminators (MSB clear) among this lane's valid bytes
-    uint32_t cnt = 0;
+    // terminators (MSB clear) among this lane's valid bytes: 64-bit mask + popcount
+    const int64_t p0 = kC - 32 + 64 * tid;
+    const int vlo = (int)max((int64_t)0, start - p0);
+    const int vhi = (int)min((int64_t)64, end - p0);
+    uint64_t vmask = 0;
+    if (vhi > vlo) vmask = (vhi >= 64 ? ~0ull : ((1ull << vhi) - 1)) & ~((1ull << vlo) - 1);
+    uint64_t tmask = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int off = 64 * tid + 16 * q;
-      const uint4 d = *reinterpret_cast<const uint4*>(buf + off);
+      const uint4 d = *reinterpret_cast<const uint4*>(buf + 64 * tid + 16 * q);
       const uint32_t ws[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
-      for (int bb = 0; bb < 16; ++bb) {
-        const int64_t pos = kC - 32 + off + bb;
-        const uint32_t byte = (ws[bb >> 2] >> ((bb & 3) * 8)) & 0xff;
-        cnt += (pos >= start && pos < end && !(byte & 0x80)) ? 1u : 0u;
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t t = ~ws[u] & 0x80808080u;
+        const uint64_t bits = ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+        tmask |= bits << (16 * q + 4 * u);
       }
     }
+    const uint32_t cnt = (uint32_t)__popcll(tmask & vmask);
     const uint32_t tot = block_sum(cnt, scratch);
     if (tid == 0) term_cnt[(size_t)j * K + k] = tot;
     // store plaintext in place (bytes past `end` land in the slot padding)
