@@ -128,6 +128,8 @@ class SdaClient {
 
   const Agent& agent() const { return agent_; }
   SdaService& service() { return *service_; }
+  ServicePtr service_ptr() const { return service_; }
+  StorePtr keystore() const { return keystore_; }
 
   // Maintenance
   void upload_agent();

@@ -39,18 +39,36 @@ SDA_DEV uint32_t canon_varint(uint64_t z, const ModParams& mp, bool& bad) {
   return r == 0 ? 0u : mp.m - r;
 }
 
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+
+// Two candidate values from a word holding two (previous byte, byte) pairs in
+// its 16-bit halves: z = prev-is-continuation ? byte<<7 | prev&0x7f : byte,
+// then zigzag-decode and reduce a value in (-m, m) into [0, m). Halves whose
+// byte is not a terminator produce garbage the caller discards.
+SDA_DEV uint32_t pair_values(uint32_t P, u16x2 mpair) {
+  const uint32_t z2 = ((P >> 1) & 0x7f807f80u) | (P & 0x007f007fu);
+  const uint32_t z1 = (P >> 8) & 0x00ff00ffu;
+  const uint32_t sel = ((P >> 7) & 0x00010001u) * 0xffffu;
+  const uint32_t z = (sel & z2) | (~sel & z1);
+  const uint32_t neg = z & 0x00010001u;
+  const uint32_t u = ((z >> 1) & 0x7fff7fffu) + neg;  // |value|, no carry across halves
+  const uint32_t nsel = neg * 0xffffu;
+  const uint32_t mu = __builtin_bit_cast(uint32_t, mpair - __builtin_bit_cast(u16x2, u));
+  return (nsel & mu) | (~nsel & u);
+}
+
 // One block per (chunk, message). Each lane owns 64 plaintext bytes held in
 // registers; terminator positions are a 64-bit mask (popcount -> block scan ->
-// ranks), the varint straddling into a lane is carried in by looking back <= 9
-// bytes in LDS, and decoded values are staged in LDS so the global store of the
-// chunk's contiguous element range is coalesced.
+// ranks); the bytes preceding a lane come from its neighbour by a shuffle (lane
+// 0 of a wave loads them); decoded values are staged in LDS so the global store
+// of the chunk's contiguous element range is coalesced. Varints of 3+ bytes
+// (large moduli, ChaCha seeds) walk back through global memory.
 template <typename VT>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
     k_decode(int L, ModParams mp, const uint8_t* __restrict__ pt, uint64_t stride,
              const uint32_t* __restrict__ pt_len, const uint32_t* __restrict__ elem_start,
              VT* __restrict__ vals, uint32_t* err) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kChunkBytes + 16];
-  __shared__ VT outb[kChunkBytes];
+  __shared__ VT outb[kChunkBytes + 128];  // + a dummy dword per wave lane
   __shared__ uint32_t scratch[kWaves];
   const int k = blockIdx.x, j = blockIdx.y, K = gridDim.x;
   const int tid = threadIdx.x;
@@ -67,11 +85,12 @@ __global__ void __launch_bounds__(kBlock)
     const int64_t pos = p0 + 16 * q;
     uint4 d = make_uint4(0, 0, 0, 0);
     if (pos >= 0 && pos < end) d = *reinterpret_cast<const uint4*>(gmsg + pos);
-    *reinterpret_cast<uint4*>(buf + 16 + 64 * tid + 16 * q) = d;
     w[4 * q] = d.x; w[4 * q + 1] = d.y; w[4 * q + 2] = d.z; w[4 * q + 3] = d.w;
   }
-  if (tid == 0 && kC - 48 >= 0)
-    *reinterpret_cast<uint4*>(buf) = *reinterpret_cast<const uint4*>(gmsg + kC - 48);
+  // the 4 bytes before this lane's range, for lane 0 of each wave (the other
+  // lanes take them from their neighbour below)
+  uint32_t wave_prev = 0;
+  if ((tid & 63) == 0 && p0 - 4 >= 0 && p0 - 4 < end) wave_prev = *reinterpret_cast<const uint32_t*>(gmsg + p0 - 4);
   // valid bytes [lo, hi) of this lane
   const int lo = (int)max((int64_t)0, start - p0);
   const int hi = (int)min((int64_t)64, end - p0);
@@ -87,75 +106,121 @@ __global__ void __launch_bounds__(kBlock)
     const uint64_t bits = ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
     tmask |= bits << (4 * i);
   }
+  const uint64_t traw = tmask;
   tmask &= vmask;
   uint32_t total;
   uint32_t local = block_excl_scan((uint32_t)__popcll(tmask), scratch, &total);  // syncs
   bool bad = false;
-  const int64_t img = 16 - (kC - 32);  // LDS index of message position 0
   // The two bytes preceding this lane's range (previous lane's last word; lane 0
   // of each wave reads them from the LDS image, which holds the chunk prefix).
   uint32_t prev_word = __shfl_up(w[15], 1, 64);
-  if ((tid & 63) == 0) {
-    const int64_t q = p0 - 4;
-    prev_word = 0;
-    for (int u = 0; u < 4; ++u) {
-      const int64_t pos = q + u;
-      const uint32_t byte = (pos >= 0 && pos >= kC - 48) ? buf[img + pos] : 0u;
-      prev_word |= byte << (8 * u);
-    }
-  }
-  // Static pass over the 64 bytes, all in registers (the LDS image is only
-  // touched by the rare long-varint walk: lanes 64 B apart would all hit the
-  // same two LDS banks). A terminator at b closes a 1-, 2- or 3-byte varint
-  // depending on the continuation bits of bytes b-1, b-2; four bytes and more
-  // (|value| >= 2^20) take the LDS walk below.
-  uint32_t long_mask_lo = 0, long_mask_hi = 0;  // terminators needing the slow path
-  uint32_t b3 = (prev_word >> 8) & 0xffu, b2 = (prev_word >> 16) & 0xffu, b1 = prev_word >> 24;
+  if ((tid & 63) == 0) prev_word = wave_prev;
+  // Fast path (u16 values, modulus < 2^16, no varint longer than two bytes,
+  // canonical range): SWAR over 16-bit halves -- one 32-bit op yields the
+  // candidate values of two byte positions. Odd positions pair with the byte
+  // before them inside the same half of the word; even positions use the word
+  // realigned by one byte (v_alignbyte). Every position then stores its
+  // candidate, non-terminators into a per-lane dummy slot. A lane that meets a
+  // longer varint or an out-of-range value re-runs the generic path below.
+  const uint32_t local0 = local;
+  const uint32_t dummy = kChunkBytes + 2 * (tid & 63);  // own dword per lane of a wave
+  const uint32_t tmask_lo = (uint32_t)tmask, tmask_hi = (uint32_t)(tmask >> 32);
+  bool redo = true;
+  if constexpr (sizeof(VT) == 2) {
+    if (mp.m != 0 && mp.m < 65536u) {
+      const uint64_t craw = ~traw;  // continuation bytes
+      const uint32_t cm1 = prev_word >> 31, cm2 = (prev_word >> 23) & 1u;
+      const bool longv = (craw & (craw << 1)) != 0 || (cm1 & ((uint32_t)craw & 1u)) || (cm1 & cm2);
+      const u16x2 mpair = {(uint16_t)mp.m, (uint16_t)mp.m};
+      u16x2 vmax = {0, 0};
+      uint32_t wp = prev_word;
 #pragma unroll
-  for (int b = 0; b < 64; ++b) {
-    const uint32_t byte = (w[b >> 2] >> (8 * (b & 3))) & 0xffu;
-    if ((tmask >> b) & 1) {
-      uint64_t z;
-      if (!(b1 & 0x80)) {
-        z = byte;
-      } else if (!(b2 & 0x80)) {
-        z = (b1 & 0x7f) | (byte << 7);
-      } else {
-        z = (b2 & 0x7f) | ((b1 & 0x7f) << 7) | (byte << 14);
-        if (b3 & 0x80) {
-          if (b < 32) long_mask_lo |= 1u << b; else long_mask_hi |= 1u << (b - 32);
-        }
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t W = w[i];
+        const uint32_t Pe = __builtin_amdgcn_alignbyte(W, wp, 3);  // [wp.B3 W.B0 | W.B1 W.B2]
+        const uint32_t ve = pair_values(Pe, mpair), vo = pair_values(W, mpair);
+        const uint32_t t4 = ((i < 8 ? tmask_lo : tmask_hi) >> (4 * (i & 7))) & 15u;
+        const uint32_t te = ((t4 & 1u) * 0xffffu) | (((t4 >> 2) & 1u) * 0xffff0000u);
+        const uint32_t to = (((t4 >> 1) & 1u) * 0xffffu) | (((t4 >> 3) & 1u) * 0xffff0000u);
+        vmax = __builtin_elementwise_max(vmax, __builtin_bit_cast(u16x2, ve & te));
+        vmax = __builtin_elementwise_max(vmax, __builtin_bit_cast(u16x2, vo & to));
+        uint32_t t;
+        t = t4 & 1u;        outb[t ? local : dummy] = (VT)ve;         local += t;
+        t = (t4 >> 1) & 1u; outb[t ? local : dummy] = (VT)vo;         local += t;
+        t = (t4 >> 2) & 1u; outb[t ? local : dummy] = (VT)(ve >> 16); local += t;
+        t = (t4 >> 3) & 1u; outb[t ? local : dummy] = (VT)(vo >> 16); local += t;
+        wp = W;
       }
-      outb[local] = (VT)canon_varint(z, mp, bad);
-      ++local;
+      redo = longv || vmax.x >= mp.m || vmax.y >= mp.m;
     }
-    b3 = b2;
-    b2 = b1;
-    b1 = byte;
   }
-  // rare slow path: rewrite the values of >= 3-byte varints
-  uint64_t lm = ((uint64_t)long_mask_hi << 32) | long_mask_lo;
-  if (lm) {
-    uint32_t rank0 = local - (uint32_t)__popcll(tmask);
-    while (lm) {
-      const int b = __builtin_ctzll(lm);
-      lm &= lm - 1;
-      const uint32_t r = rank0 + (uint32_t)__popcll(tmask & ((1ull << b) - 1));
-      const int64_t q = p0 + b;
-      int64_t s0 = q;
-      int n = 0;
-      while (n < 10 && s0 > 0 && (buf[img + s0 - 1] & 0x80)) { --s0; ++n; }
-      bad |= n >= 10;
-      uint64_t z = 0;
-      for (int64_t u = s0; u <= q; ++u) {
-        const uint32_t sh = 7u * (uint32_t)(u - s0);
-        if (sh < 64) z |= (uint64_t)(buf[img + u] & 0x7f) << sh;
+  if (redo) {
+    // Generic path, all in registers (the LDS image is only touched by the
+    // rare long-varint walk: lanes 64 B apart would all hit the same two LDS
+    // banks). A terminator at b closes a 1-, 2- or 3-byte varint depending on
+    // the continuation bits of bytes b-1, b-2; four bytes and more
+    // (|value| >= 2^20) take the LDS walk.
+    // opaque copies: stop the compiler from sharing (and keeping live across
+    // the fast path) the per-byte terms it would otherwise CSE between paths
+    uint32_t tlo = tmask_lo, thi = tmask_hi;
+    local = local0;
+    asm volatile("" : "+v"(tlo), "+v"(thi), "+v"(local));
+    uint32_t long_mask_lo = 0, long_mask_hi = 0;  // terminators needing the slow path
+    uint32_t b3 = (prev_word >> 8) & 0xffu, b2 = (prev_word >> 16) & 0xffu, b1 = prev_word >> 24;
+    // Branch-free: every byte stores a value, non-terminators into a per-lane
+    // dummy slot, so the unrolled loop compiles to straight-line VALU + ds_write.
+    // Conditions are kept as integer 0/1 / all-ones masks (bools become SGPR
+    // lane masks that the compiler then spills across the unrolled loop).
+    uint32_t neg_raw = 0;
+  #pragma unroll
+    for (int b = 0; b < 64; ++b) {
+      const uint32_t byte = (w[b >> 2] >> (8 * (b & 3))) & 0xffu;
+      const uint32_t term = ((b < 32 ? tlo : thi) >> (b & 31)) & 1u;
+      const uint32_t c1 = b1 >> 7, c2 = b2 >> 7, c3 = b3 >> 7;
+      const uint32_t m1 = 0u - c1, m2 = 0u - c2;
+      const uint32_t z2 = (b1 & 0x7f) | (byte << 7);
+      const uint32_t z3 = (b2 & 0x7f) | ((b1 & 0x7f) << 7) | (byte << 14);
+      const uint32_t z = (byte & ~m1) | (z2 & m1 & ~m2) | (z3 & m1 & m2);  // < 2^21
+      const uint32_t lng = term & c1 & c2 & c3;
+      if (b < 32) long_mask_lo |= lng << b; else long_mask_hi |= lng << (b - 32);
+      const uint32_t neg = z & 1u;
+      const uint32_t u = (z >> 1) + neg;  // |value| (value = -u when neg)
+      const uint32_t r = mod32(u, mp);    // m == 0: raw
+      const uint32_t nr = r == 0 ? 0u : mp.m - r;
+      const uint32_t v = r ^ ((r ^ nr) & (0u - neg));
+      neg_raw |= term & neg & (lng ^ 1u);
+      const uint32_t addr = dummy ^ ((dummy ^ local) & (0u - term));
+      outb[addr] = (VT)v;
+      local += term;
+      b3 = b2;
+      b2 = b1;
+      b1 = byte;
+    }
+    if (mp.m == 0) bad |= neg_raw != 0;  // a raw (modulus-free) stream holds no negatives
+    // rare slow path: rewrite the values of >= 3-byte varints
+    uint64_t lm = ((uint64_t)long_mask_hi << 32) | long_mask_lo;
+    if (lm) {
+      uint32_t rank0 = local - (uint32_t)__popcll(tmask);
+      while (lm) {
+        const int b = __builtin_ctzll(lm);
+        lm &= lm - 1;
+        const uint32_t r = rank0 + (uint32_t)__popcll(tmask & ((1ull << b) - 1));
+        const int64_t q = p0 + b;
+        int64_t s0 = q;
+        int n = 0;
+        while (n < 10 && s0 > 0 && (gmsg[s0 - 1] & 0x80)) { --s0; ++n; }
+        bad |= n >= 10;
+        uint64_t z = 0;
+        for (int64_t u = s0; u <= q; ++u) {
+          const uint32_t sh = 7u * (uint32_t)(u - s0);
+          if (sh < 64) z |= (uint64_t)(gmsg[u] & 0x7f) << sh;
+        }
+        outb[r] = (VT)canon_varint(z, mp, bad);
       }
-      outb[r] = (VT)canon_varint(z, mp, bad);
     }
   }
   // a message must end on a terminator
-  if (hi > lo && p0 + hi == (int64_t)N && (buf[img + N - 1] & 0x80)) bad = true;
+  if (hi > lo && p0 + hi == (int64_t)N && (gmsg[N - 1] & 0x80)) bad = true;
   __syncthreads();
   const uint32_t base = elem_start[(size_t)j * K + k];
   VT* out = vals + (size_t)j * L;

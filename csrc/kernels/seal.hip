@@ -18,7 +18,6 @@
 namespace sdagpu {
 namespace {
 
-constexpr int kLdsEncodeBytes = kEncodeValues * 5 + 128;
 constexpr int kValuesPerLane = kEncodeValues / kBlock;  // 32
 
 template <typename VT>
@@ -56,7 +55,8 @@ template <typename VT>
 __global__ void __launch_bounds__(kBlock)
     k_encode_encrypt(int L, const VT* __restrict__ vals, const uint32_t* __restrict__ tile_off,
                      const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct, uint64_t stride) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEncodeBytes];
+  // u16 values are at most 3-byte varints, u32 at most 5
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kEncodeValues * (sizeof(VT) == 2 ? 3 : 5) + 128];
   __shared__ uint32_t scratch[kWaves];
   const int t = blockIdx.x, j = blockIdx.y;
   const int T = (L + kTileValues - 1) / kTileValues;  // count tiles per message
@@ -66,12 +66,25 @@ __global__ void __launch_bounds__(kBlock)
   const bool vec_ok = ((size_t)L * sizeof(VT)) % 16 == 0;
   uint32_t v[kValuesPerLane];
   load_values<VT>(v, src, e0, L, vec_ok);
-  uint32_t my_bytes = 0;
+  // Fast lanes (all 32 values present and < 2^13, i.e. 1- or 2-byte varints):
+  // branch-free encode, each value stores both candidate bytes and the next
+  // value overwrites the second one when the varint was a single byte (same
+  // lane, so LDS program order holds). Other lanes take the generic path.
+  uint32_t orv = 0;
 #pragma unroll
-  for (int i = 0; i < kValuesPerLane; ++i) {
-    const uint64_t z = (uint64_t)v[i] << 1;
-    const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
-    my_bytes += (e0 + i < L) ? len : 0u;
+  for (int i = 0; i < kValuesPerLane; ++i) orv |= v[i];
+  const bool fast = (e0 + kValuesPerLane <= L) && orv < 8192u;
+  uint32_t my_bytes = 0;
+  if (fast) {
+#pragma unroll
+    for (int i = 0; i < kValuesPerLane; ++i) my_bytes += 1u + (v[i] >= 64u);
+  } else {
+#pragma unroll
+    for (int i = 0; i < kValuesPerLane; ++i) {
+      const uint64_t z = (uint64_t)v[i] << 1;
+      const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
+      my_bytes += (e0 + i < L) ? len : 0u;
+    }
   }
   uint32_t tile_bytes;
   const uint32_t excl = block_excl_scan(my_bytes, scratch, &tile_bytes);
@@ -79,16 +92,27 @@ __global__ void __launch_bounds__(kBlock)
   const uint32_t b0 = (32u + a) >> 6;
   const uint32_t base = 32u + a - 64u * b0;  // LDS index of message byte `a`
   uint32_t pos = base + excl;
+  if (fast) {
 #pragma unroll
-  for (int i = 0; i < kValuesPerLane; ++i) {
-    if (e0 + i < L) {
-      const uint64_t z = (uint64_t)v[i] << 1;
-      const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
+    for (int i = 0; i < kValuesPerLane; ++i) {
+      const uint32_t z = v[i] << 1;
+      const uint32_t l2 = v[i] >= 64u;
+      lds[pos] = (uint8_t)((z & 0x7fu) | (l2 << 7));
+      if (i + 1 < kValuesPerLane || l2) lds[pos + 1] = (uint8_t)(z >> 7);
+      pos += 1u + l2;
+    }
+  } else {
 #pragma unroll
-      for (int q = 0; q < 5; ++q)
-        if ((uint32_t)q < len)
-          lds[pos + q] = (uint8_t)(((z >> (7 * q)) & 0x7f) | ((uint32_t)q + 1 < len ? 0x80u : 0u));
-      pos += len;
+    for (int i = 0; i < kValuesPerLane; ++i) {
+      if (e0 + i < L) {
+        const uint64_t z = (uint64_t)v[i] << 1;
+        const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+          if ((uint32_t)q < len)
+            lds[pos + q] = (uint8_t)(((z >> (7 * q)) & 0x7f) | ((uint32_t)q + 1 < len ? 0x80u : 0u));
+        pos += len;
+      }
     }
   }
   __syncthreads();
