@@ -312,21 +312,28 @@ void HttpServer::stop() {
 }
 
 // ---- REST router ----------------------------------------------------------------
+// Deviation: the reference answers 500 for a missing / malformed header (its
+// errors are plain strings there); here they are InvalidCredentials -> 401.
 AuthToken parse_basic_auth(const std::string& header_value) {
+  auto fail = [](const char* why) { return SdaError(ErrorKind::InvalidCredentials, why); };
   std::string h = trim(header_value);
-  if (h.empty()) throw SdaError("Mandatory Authorization header");
-  if (h.rfind("Basic ", 0) != 0) throw SdaError("Basic Authorization required");
+  if (h.empty()) throw fail("Mandatory Authorization header");
+  if (h.rfind("Basic ", 0) != 0) throw fail("Basic Authorization required");
   Bytes dec;
   try {
     dec = base64_decode(trim(h.substr(6)));
   } catch (const SdaError&) {
-    throw SdaError("Invalid Auth header (base64)");
+    throw fail("Invalid Auth header (base64)");
   }
   std::string s(dec.begin(), dec.end());
   auto c = s.find(':');
-  if (c == std::string::npos) throw SdaError("Invalid Auth header");
+  if (c == std::string::npos) throw fail("Invalid Auth header");
   AuthToken t;
-  t.id = AgentId::parse(s.substr(0, c));
+  try {
+    t.id = AgentId::parse(s.substr(0, c));
+  } catch (const SdaError&) {
+    throw fail("Invalid Auth header (agent id)");
+  }
   t.body = s.substr(c + 1);
   return t;
 }

@@ -304,7 +304,8 @@ class KvAggregationsStore : public AggregationsStore {
     if (!content) throw SdaError("snapshot content not found");
     auto parts = participations(aggregation);
     std::vector<Participation> out;
-    for (auto& id : json::Value::parse(*content).at("participations").as_array()) {
+    const json::Value doc = json::Value::parse(*content);  // keep alive across the loop
+    for (auto& id : doc.at("participations").as_array()) {
       auto p = get_as<Participation>(*parts, id.as_string());
       if (!p) throw SdaError("participation id=" + id.as_string() + " not found");
       out.push_back(std::move(*p));
@@ -327,7 +328,8 @@ class KvAggregationsStore : public AggregationsStore {
     auto v = masks_->get(s.str());
     if (!v) return std::nullopt;
     std::vector<Encryption> out;
-    for (auto& e : json::Value::parse(*v).as_array()) out.push_back(wire::from_json<Encryption>(e));
+    const json::Value doc = json::Value::parse(*v);
+    for (auto& e : doc.as_array()) out.push_back(wire::from_json<Encryption>(e));
     return out;
   }
 

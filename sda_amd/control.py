@@ -30,7 +30,7 @@ def _c():
 
 
 def _enc(obj: Any) -> str:
-    return obj if isinstance(obj, str) else json.dumps(obj, separators=(",", ":"))
+    return json.dumps(obj, separators=(",", ":"))
 
 
 def _dec(text: Optional[str]) -> Optional[Obj]:
