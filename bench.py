@@ -14,8 +14,9 @@ time (whole job: summed over all ranks).
 
 Scaling is *weak*: each rank hosts `--participants` (default 1000) participants,
 so N ranks aggregate N x 1000 x 1M elements per step. With N > 1 the round runs
-through sda_amd.parallel (RCCL all-to-all of the sealed boxes over xGMI,
-clerk partials reduced to the clerks' lead ranks, results gathered to rank 0).
+through sda_amd.parallel.DistributedAggregator ("owner computes": each rank
+seals, opens and combines its own participants' boxes for every clerk; one
+bucketed RCCL reduce of the clerk partial sums to rank 0, the recipient).
 
 Launch: python bench.py --gpus 1 --steps 5 --warmup 2
         python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -50,6 +51,8 @@ def parse():
     ap.add_argument("--modulus", type=int, default=433)
     ap.add_argument("--check", action="store_true", help="verify the output every step")
     ap.add_argument("--stages", action="store_true", help="print per-stage times (rank 0)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU")
     return ap.parse_args()
 
 
@@ -65,9 +68,13 @@ def main():
         if world == 1 and args.gpus > 1:
             print("bench.py: launch with torch.distributed.run for --gpus > 1", file=sys.stderr)
             sys.exit(2)
-    torch.cuda.set_device(local_rank)
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
 
     from sda_amd.models.schemes import Additive, AggregationSpec, NoMask
 
@@ -91,12 +98,16 @@ def main():
     else:
         from sda_amd.parallel.engine import DistributedAggregator
 
-        agg = DistributedAggregator(spec, participants_per_rank=P, time_stages=args.stages)
+        agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", dev_index),
+                                    time_stages=args.stages)
 
         def step(check):
             return agg.run_round(secrets, check=check)
 
         expected = None
+        # the global reference sum, reduced to rank 0, validates the first warmup round
+        local = agg.comm.reduce_sum(secrets.to(torch.int64).sum(0), dst=0)
+        global_ref = torch.remainder(local, args.modulus).to(torch.int32) if rank == 0 else None
 
     # warmup (also validates the result once)
     for i in range(args.warmup):
@@ -105,8 +116,11 @@ def main():
             ref = reference_sum(secrets, args.modulus)
             if not torch.equal(res.output, ref):
                 raise SystemExit("bench: device aggregation does not match the reference sum")
+        if i == 0 and world > 1 and rank == 0:
+            if not torch.equal(res.output, global_ref):
+                raise SystemExit("bench: distributed aggregation does not match the reference sum")
     if world > 1:
-        dist.barrier()
+        agg.comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -115,12 +129,10 @@ def main():
             raise SystemExit("bench: mismatch")
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        agg.comm.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = agg.comm.all_reduce_max(elapsed)
     ms = elapsed / args.steps * 1e3
     total_elems = P * world * args.dim
     value = total_elems / (ms / 1e3)
@@ -148,7 +160,8 @@ def main():
                 "participants_per_gpu": P,
                 "dimension": args.dim,
                 "clerks": args.clerks,
-                "parallelism": f"participants sharded x{world}, clerk jobs all-to-all" if world > 1
+                "parallelism": (f"dp{world}: participants sharded over {world} GPUs, clerk "
+                                "partials reduced to rank 0 over RCCL") if world > 1
                                else "single GPU",
             },
         }

@@ -138,7 +138,7 @@ class DeviceAggregator:
         return self._side
 
     def run_round(self, secrets: torch.Tensor, clerks: Sequence[int] | None = None,
-                  check: bool = True) -> RoundResult:
+                  check: bool = True, reducer=None, owner_base: int = 0) -> RoundResult:
         """One full round for participant vectors `secrets` [P][D] (int32, on device).
 
         Stream schedule: every X25519 / key-derivation kernel (participants'
@@ -146,6 +146,13 @@ class DeviceAggregator:
         stream concurrently with the bandwidth-bound share/encode/MAC kernels of
         the main stream; the main stream waits on events only where it consumes
         derived keys.
+
+        `reducer(partials) -> reduced | None` (multi-GPU): called with the
+        per-clerk column sums over this device's participants -- int64
+        [len(live) (+1 with a mask)][B or D] -- before the recipient stage; it
+        returns the sums over all devices on the root and None elsewhere (which
+        then skips the recipient stage and returns ``output=None``).
+        `owner_base` offsets the participants' RNG stream ids.
         """
         spec, n, m = self.spec, self.n, self.m
         if secrets.dim() != 2 or secrets.shape[1] != spec.dimension:
@@ -204,14 +211,14 @@ class DeviceAggregator:
                 t.record_stream(main)
 
         # ---- participants: mask + share, then encrypt (waits for the seal keys)
-        shares, cnt, mask_vals, mask_cnt = self._share(secrets, rng_key, 0, err)
+        shares, cnt, mask_vals, mask_cnt = self._share(secrets, rng_key, owner_base, err)
         main.wait_event(ev_sealkeys)
         seal_data(clerk_arena, ks_clerk, shares.view(n * P, B), err, cnt)
         if mask_arena is not None:
             seal_data(mask_arena, ks_mask, mask_vals, err, mask_cnt)
         self._mark(marks, "participate")
 
-        # ---- clerks: verify + decrypt + decode their P boxes, combine, reseal
+        # ---- clerks: verify + decrypt + decode their P boxes, combine
         main.wait_event(ev_openkeys)
         if len(live) == n:
             vals = open_data(clerk_arena, ko_clerk[0], err, out_dtype=self.vdtype)
@@ -221,9 +228,37 @@ class DeviceAggregator:
                 open_data(clerk_arena.slice(c * P, P), ko_clerk[i], err, out=vals[i])
         combined = torch.empty(len(live), B, dtype=torch.int32, device=dev)
         G.colsum(vals.view(len(live), P, B), m, combined)
+        # recipient's share of the mask work is data-parallel too: open this
+        # device's participants' mask boxes and sum them
+        mask_sum = None
+        if mask_arena is not None:
+            mask_sum = torch.empty(D, dtype=torch.int32, device=dev)
+            mvals = open_data(mask_arena, ko_mask, err, out_dtype=torch.int32)
+            if isinstance(spec.masking, FullMask):
+                G.colsum(mvals.view(1, P, D), m, mask_sum)
+            else:
+                G.chacha_mask_sum(mvals, D, m, mask_sum, err)
+        self._mark(marks, "clerk")
+
+        if reducer is not None:
+            # one bucket: clerk sums (B wide) and the mask sum (D wide) as rows
+            nrow = len(live) + (1 if mask_sum is not None else 0)
+            partials = torch.zeros(nrow, max(B, D), dtype=torch.int64, device=dev)
+            partials[:len(live), :B] = combined
+            if mask_sum is not None:
+                partials[len(live), :D] = mask_sum
+            reduced = reducer(partials)
+            self._mark(marks, "reduce")
+            if reduced is None:
+                return self._finish(err, marks, check, RoundResult(None, live, {}))
+            reduced = torch.remainder(reduced, m).to(torch.int32)
+            combined = reduced[:len(live), :B].contiguous()
+            if mask_sum is not None:
+                mask_sum = reduced[len(live), :D].contiguous()
+
+        # ---- clerks reseal their results for the recipient
         res_vals = combined if self.vdtype == torch.int32 else combined.to(self.vdtype)
         seal_data(res_arena, ks_res, res_vals, err)
-        self._mark(marks, "clerk")
 
         # ---- recipient: open results, reconstruct, unmask
         ys = open_data(res_arena, ko_res, err, out_dtype=torch.int32)
@@ -234,25 +269,20 @@ class DeviceAggregator:
             lag = self._lagrange(live)
             G.pss_reconstruct(ys, lag, spec.sharing.secret_count, D, m, masked)
         out = masked
-        if mask_arena is not None:
-            mask_sum = torch.empty(D, dtype=torch.int32, device=dev)
-            mvals = open_data(mask_arena, ko_mask, err, out_dtype=torch.int32)
-            if isinstance(spec.masking, FullMask):
-                G.colsum(mvals.view(1, P, D), m, mask_sum)
-            else:
-                G.chacha_mask_sum(mvals, D, m, mask_sum, err)
+        if mask_sum is not None:
             out = torch.empty(D, dtype=torch.int32, device=dev)
             G.sub_mod(masked, mask_sum, m, out)
         self._mark(marks, "reveal")
+        return self._finish(err, marks, check, RoundResult(out, live, {}))
 
-        stage_ms = {}
+    def _finish(self, err, marks, check, result: RoundResult) -> RoundResult:
         if check or self.time_stages:
             e = int(err.item())
             if e:
                 raise AggregationError(f"device error word 0x{e:x} ({describe_error(e)})")
             for (a, ea), (b, eb) in zip(marks, marks[1:]):
-                stage_ms[b] = ea.elapsed_time(eb)
-        return RoundResult(out, live, stage_ms)
+                result.stage_ms[b] = ea.elapsed_time(eb)
+        return result
 
     def _lagrange(self, live):
         key = tuple(live)

@@ -19,6 +19,9 @@ class NoMask:
     def has_mask(self) -> bool:
         return False
 
+    def to_wire(self):
+        return "None"
+
 
 @dataclass(frozen=True)
 class FullMask:
@@ -27,6 +30,9 @@ class FullMask:
 
     def has_mask(self) -> bool:
         return True
+
+    def to_wire(self):
+        return {"Full": {"modulus": self.modulus}}
 
 
 @dataclass(frozen=True)
@@ -42,6 +48,10 @@ class ChaChaMask:
     @property
     def seed_words(self) -> int:
         return (self.seed_bitsize + 31) // 32
+
+    def to_wire(self):
+        return {"ChaCha": {"modulus": self.modulus, "dimension": self.dimension,
+                           "seed_bitsize": self.seed_bitsize}}
 
 
 MaskingScheme = Union[NoMask, FullMask, ChaChaMask]
@@ -69,6 +79,9 @@ class Additive:
     def field_modulus(self) -> int:
         return self.modulus
 
+    def to_wire(self):
+        return {"Additive": {"share_count": self.share_count, "modulus": self.modulus}}
+
 
 @dataclass(frozen=True)
 class PackedShamir:
@@ -95,6 +108,14 @@ class PackedShamir:
     @property
     def field_modulus(self) -> int:
         return self.prime_modulus
+
+    def to_wire(self):
+        return {"PackedShamir": {"secret_count": self.secret_count,
+                                 "share_count": self.share_count,
+                                 "privacy_threshold": self.privacy_threshold_,
+                                 "prime_modulus": self.prime_modulus,
+                                 "omega_secrets": self.omega_secrets,
+                                 "omega_shares": self.omega_shares}}
 
     def native(self):
         from .._native import native

@@ -1,0 +1,74 @@
+"""Collectives for the aggregation engines.
+
+With the ``nccl`` backend (RCCL on ROCm, over xGMI) tensors stay on the GPU.
+With ``gloo`` (CPU tests, or several ranks sharing one GPU) device tensors are
+staged through host memory, so the same engine code runs on both.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self, group=None):
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed is not initialised")
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+        self.device_native = self.backend == "nccl"
+
+    # -- staging helpers ------------------------------------------------------
+    def _to_wire(self, t):
+        if isinstance(t, np.ndarray):
+            return torch.from_numpy(np.ascontiguousarray(t)), "numpy", None
+        if t.is_cuda and not self.device_native:
+            return t.cpu(), "cuda", t.device
+        return t, "torch", None
+
+    @staticmethod
+    def _from_wire(w, kind, device):
+        if kind == "numpy":
+            return w.numpy()
+        if kind == "cuda":
+            return w.to(device)
+        return w
+
+    # -- collectives ------------------------------------------------------------
+    def barrier(self):
+        if self.device_native:
+            dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier(group=self.group)
+
+    def broadcast(self, t, src: int = 0):
+        w, kind, dev = self._to_wire(t)
+        dist.broadcast(w, src=src, group=self.group)
+        return self._from_wire(w, kind, dev)
+
+    def reduce_sum(self, t, dst: int = 0):
+        """Sum over ranks; the result on `dst`, None elsewhere."""
+        w, kind, dev = self._to_wire(t)
+        w = w.contiguous()
+        dist.reduce(w, dst=dst, op=dist.ReduceOp.SUM, group=self.group)
+        return self._from_wire(w, kind, dev) if self.rank == dst else None
+
+    def all_reduce_max(self, value: float) -> float:
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.device_native else "cpu"
+        t = torch.tensor([value], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+    def all_to_all_equal(self, out: torch.Tensor, inp: torch.Tensor):
+        """Equal-split all-to-all of a flat buffer (rank r gets block r of every rank)."""
+        w_in, kind, dev = self._to_wire(inp)
+        if kind == "cuda":
+            w_out = torch.empty_like(w_in)
+            dist.all_to_all_single(w_out, w_in, group=self.group)
+            out.copy_(w_out.to(dev))
+        else:
+            dist.all_to_all_single(out, w_in, group=self.group)
+        return out

@@ -1,0 +1,66 @@
+"""Distributed device engine on one GPU: two ranks share cuda:0 over gloo
+(device tensors staged through host memory). Exercises the same
+DistributedAggregator + DeviceAggregator code that runs one rank per MI355X
+over RCCL; rank 0 compares with the plain PyTorch sum of both ranks' inputs.
+"""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, name, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from sda_amd.models.schemes import PSS_4_8_3, Additive, AggregationSpec, FullMask
+        from sda_amd.parallel import DistributedAggregator
+
+        D, P, m = 5000, 6, 433
+        spec = (AggregationSpec(D, m, Additive(3, m), FullMask(m)) if name == "fullmask"
+                else AggregationSpec(D, m, PSS_4_8_3))
+        agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", 0))
+
+        def inputs(r):
+            g = torch.Generator().manual_seed(99 + r)
+            return torch.randint(0, m, (P, D), dtype=torch.int32, generator=g)
+
+        res = agg.run_round(inputs(rank).cuda())
+        if rank == 0:
+            ref = torch.remainder(sum(inputs(r).to(torch.int64).sum(0) for r in range(world)), m)
+            q.put(("ok", bool(torch.equal(res.output.cpu().to(torch.int64), ref))))
+        else:
+            q.put(("ok", res.output is None))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", f"rank {rank}: {type(e).__name__}: {e}"))
+
+
+@pytest.mark.parametrize("name", ["fullmask", "pss"])
+def test_distributed_device_two_ranks_one_gpu(cuda, name):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [r[1] for r in results if r[0] == "err"]
+    assert not errs, errs
+    assert all(r[1] for r in results), results
