@@ -14,9 +14,11 @@ time (whole job: summed over all ranks).
 
 Scaling is *weak*: each rank hosts `--participants` (default 1000) participants,
 so N ranks aggregate N x 1000 x 1M elements per step. With N > 1 the round runs
-through sda_amd.parallel.DistributedAggregator ("owner computes": each rank
-seals, opens and combines its own participants' boxes for every clerk; one
-bucketed RCCL reduce of the clerk partial sums to rank 0, the recipient).
+through sda_amd.parallel.DistributedAggregator: by default the committee layout
+(each rank seals its participants' boxes; the snapshot transpose routes them
+over xGMI to the ranks playing the clerks, with no rank holding two clerks'
+shares of a participant; clerk partial sums are reduced to rank 0, the
+recipient). `--layout owner` skips the routing (upper bound).
 
 Launch: python bench.py --gpus 1 --steps 5 --warmup 2
         python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -53,6 +55,9 @@ def parse():
     ap.add_argument("--modulus", type=int, default=433)
     ap.add_argument("--check", action="store_true", help="verify the output every step")
     ap.add_argument("--stages", action="store_true", help="print per-stage times (rank 0)")
+    ap.add_argument("--layout", default="committee", choices=["committee", "owner"],
+                    help="committee: boxes routed to the clerks' GPUs (protocol trust model); "
+                         "owner: each GPU opens its own participants' boxes (upper bound)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU")
     return ap.parse_args()
@@ -101,7 +106,7 @@ def main():
         from sda_amd.parallel.engine import DistributedAggregator
 
         agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", dev_index),
-                                    time_stages=args.stages)
+                                    time_stages=args.stages, layout=args.layout)
 
         def step(check):
             return agg.run_round(secrets, check=check)
@@ -162,9 +167,11 @@ def main():
                 "participants_per_gpu": P,
                 "dimension": args.dim,
                 "clerks": args.clerks,
-                "parallelism": (f"dp{world}: participants sharded over {world} GPUs, clerk "
-                                "partials reduced to rank 0 over RCCL") if world > 1
-                               else "single GPU",
+                "parallelism": (f"dp{world} participants x committee-sharded clerks: sealed "
+                                "boxes routed over xGMI (grouped RCCL send/recv), clerk partials "
+                                "reduced to rank 0" if args.layout == "committee" else
+                                f"dp{world} owner-computes: clerk partials reduced to rank 0")
+                               if world > 1 else "single GPU",
             },
         }
         print(json.dumps(line), flush=True)

@@ -138,7 +138,8 @@ class DeviceAggregator:
         return self._side
 
     def run_round(self, secrets: torch.Tensor, clerks: Sequence[int] | None = None,
-                  check: bool = True, reducer=None, owner_base: int = 0) -> RoundResult:
+                  check: bool = True, reducer=None, owner_base: int = 0,
+                  router=None) -> RoundResult:
         """One full round for participant vectors `secrets` [P][D] (int32, on device).
 
         Stream schedule: every X25519 / key-derivation kernel (participants'
@@ -153,6 +154,9 @@ class DeviceAggregator:
         returns the sums over all devices on the root and None elsewhere (which
         then skips the recipient stage and returns ``output=None``).
         `owner_base` offsets the participants' RNG stream ids.
+        `router.exchange(arena) -> inbox` (multi-GPU committee layout): moves
+        the sealed clerk boxes to the ranks that play the clerks; the clerk
+        stage then opens the inbox (same [n][P] clerk-major shape).
         """
         spec, n, m = self.spec, self.n, self.m
         if secrets.dim() != 2 or secrets.shape[1] != spec.dimension:
@@ -198,9 +202,8 @@ class DeviceAggregator:
             ks_res = seal_setup(res_arena, kidx_rcpt_c, pks, rng_key, (n + 1) * P, err)
             ev_sealkeys = torch.cuda.Event()
             ev_sealkeys.record(side)
-            ko_clerk = [open_setup(clerk_arena.slice(c * P, P), kidx_clerk[c * P:(c + 1) * P],
-                                   sks, pks, err) for c in live] if len(live) != n else \
-                [open_setup(clerk_arena, kidx_clerk, sks, pks, err)]
+            ko_clerk = self._open_keys(clerk_arena, kidx_clerk, live, P, err) \
+                if router is None else []
             ko_res = open_setup(res_arena, kidx_rcpt_c, sks, pks, err)
             ko_mask = (open_setup(mask_arena, kidx_rcpt_p, sks, pks, err)
                        if mask_arena is not None else None)
@@ -220,12 +223,18 @@ class DeviceAggregator:
 
         # ---- clerks: verify + decrypt + decode their P boxes, combine
         main.wait_event(ev_openkeys)
+        inbox = clerk_arena
+        if router is not None:
+            # snapshot transpose over xGMI: boxes travel to the clerks' ranks
+            inbox = router.exchange(clerk_arena)
+            self._mark(marks, "exchange")
+            ko_clerk = self._open_keys(inbox, kidx_clerk, live, P, err)
         if len(live) == n:
-            vals = open_data(clerk_arena, ko_clerk[0], err, out_dtype=self.vdtype)
+            vals = open_data(inbox, ko_clerk[0], err, out_dtype=self.vdtype)
         else:
             vals = torch.empty(len(live), P, B, dtype=self.vdtype, device=dev)
             for i, c in enumerate(live):
-                open_data(clerk_arena.slice(c * P, P), ko_clerk[i], err, out=vals[i])
+                open_data(inbox.slice(c * P, P), ko_clerk[i], err, out=vals[i])
         combined = torch.empty(len(live), B, dtype=torch.int32, device=dev)
         G.colsum(vals.view(len(live), P, B), m, combined)
         # recipient's share of the mask work is data-parallel too: open this
@@ -274,6 +283,13 @@ class DeviceAggregator:
             G.sub_mod(masked, mask_sum, m, out)
         self._mark(marks, "reveal")
         return self._finish(err, marks, check, RoundResult(out, live, {}))
+
+    def _open_keys(self, arena, kidx, live, P, err):
+        pks, sks = self.keys.pks, self.keys.sks
+        if len(live) == self.n:
+            return [open_setup(arena, kidx, sks, pks, err)]
+        return [open_setup(arena.slice(c * P, P), kidx[c * P:(c + 1) * P], sks, pks, err)
+                for c in live]
 
     def _finish(self, err, marks, check, result: RoundResult) -> RoundResult:
         if check or self.time_stages:

@@ -60,7 +60,7 @@ class HostAggregator:
         self._c = native().control
 
     def run_round(self, secrets, clerks: Sequence[int] | None = None, check: bool = True,
-                  reducer=None, owner_base: int = 0) -> HostRoundResult:
+                  reducer=None, owner_base: int = 0, router=None) -> HostRoundResult:
         spec, n, m, c = self.spec, self.n, self.m, self._c
         secrets = np.asarray(secrets, dtype=np.int64)
         if secrets.ndim != 2 or secrets.shape[1] != spec.dimension:
@@ -84,12 +84,15 @@ class HostAggregator:
         t["participate"] = time.perf_counter()
 
         # clerks: open this device's participants' boxes and combine (clerk.rs:63-107)
+        # snapshot transpose: P x n -> n x P (locally, or routed to the clerks' ranks)
+        inbox = (router.exchange_host(boxes) if router is not None
+                 else [[boxes[p][j] for p in range(P)] for j in range(n)])
         combined = np.zeros((len(live), B), dtype=np.int64)
         for i, j in enumerate(live):
             kp = self.keys.keypair(j)
             acc = np.zeros(B, dtype=np.int64)
-            for p in range(P):
-                acc += np.asarray(c.decrypt_shares(kp, boxes[p][j]), dtype=np.int64)
+            for box in inbox[j]:
+                acc += np.asarray(c.decrypt_shares(kp, box), dtype=np.int64)
             combined[i] = np.remainder(acc, m)
         mask_sum = None
         if spec.masking.has_mask():

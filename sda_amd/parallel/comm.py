@@ -72,3 +72,35 @@ class Comm:
         else:
             dist.all_to_all_single(out, w_in, group=self.group)
         return out
+
+    def exchange(self, sends, recvs):
+        """Point-to-point exchange: `sends` / `recvs` are lists of (peer, tensor).
+
+        Transfers to/from the same peer are matched in list order; peer ==
+        self must not appear (callers copy locally). With RCCL the operations
+        are one grouped launch (every xGMI link busy at once); with gloo the
+        device tensors are staged through host buffers.
+        """
+        if not sends and not recvs:
+            return
+        if self.device_native:
+            ops = [dist.P2POp(dist.isend, t.contiguous(), p, group=self.group) for p, t in sends]
+            ops += [dist.P2POp(dist.irecv, t, p, group=self.group) for p, t in recvs]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+            return
+        host_sends = [(p, t.contiguous().cpu() if t.is_cuda else t.contiguous()) for p, t in sends]
+        host_recvs = [(p, torch.empty(t.shape, dtype=t.dtype) if t.is_cuda else t, t)
+                      for p, t in recvs]
+        ops = [dist.P2POp(dist.isend, t, p, group=self.group) for p, t in host_sends]
+        ops += [dist.P2POp(dist.irecv, h, p, group=self.group) for p, h, _ in host_recvs]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        for _, h, t in host_recvs:
+            if h is not t:
+                t.copy_(h)
+
+    def all_gather_object(self, obj):
+        out = [None] * self.world
+        dist.all_gather_object(out, obj, group=self.group)
+        return out

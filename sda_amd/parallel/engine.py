@@ -1,6 +1,16 @@
 """Distributed aggregation: one process per GPU, torch.distributed over RCCL/xGMI.
 
-Decomposition ("owner computes"): every rank owns a shard of the participants
+Two layouts.
+
+``committee`` (default, the protocol's trust model): every rank owns a shard of
+the participants and seals their boxes for every clerk; the snapshot transpose
+is a grouped RCCL send/recv that routes each clerk's boxes to ranks playing that
+clerk (parallel/routing.py: no rank sees two clerks' shares of a participant,
+every rank opens exactly n * P boxes, traffic spread over all xGMI peers);
+ranks open + combine their inbox per clerk; the per-clerk partial sums (clerk
+internal) and the mask partials are reduced to rank 0, the recipient.
+
+``owner`` (upper bound, *not* privacy-preserving across GPUs): every rank owns a shard of the participants
 and runs their whole pipeline locally -- mask, share, seal one box per clerk,
 and the clerks' open + combine over *its* boxes. A clerk's combine is a sum
 over participants, so each rank holds per-clerk partial sums; one bucketed
@@ -43,7 +53,7 @@ class DistributedAggregator:
     """
 
     def __init__(self, spec: AggregationSpec, engine: str = "device", device=None, group=None,
-                 time_stages: bool = False):
+                 time_stages: bool = False, layout: str = "committee"):
         self.spec = spec
         self.comm = Comm(group)
         self.rank, self.world = self.comm.rank, self.comm.world
@@ -71,6 +81,10 @@ class DistributedAggregator:
             raise ValueError("engine must be 'device' or 'host'")
         # int32 reduction is exact when the sum of `world` values < m fits
         self._narrow = self.world * (spec.field_modulus - 1) < 2 ** 31
+        if layout not in ("committee", "owner"):
+            raise ValueError("layout must be 'committee' or 'owner'")
+        self.layout = layout
+        self._routers = {}
 
     def _shared_keys(self, count: int) -> np.ndarray:
         from .._native import native
@@ -97,8 +111,23 @@ class DistributedAggregator:
         out = self.comm.reduce_sum(wire)
         return None if out is None else out.to(torch.int64)
 
+    def router(self, P: int):
+        if self.layout != "committee":
+            return None
+        if P not in self._routers:
+            from .router import CommitteeRouter
+
+            self._routers[P] = CommitteeRouter(self.comm, self.spec.n_clerks, P)
+        return self._routers[P]
+
     def run_round(self, secrets_local, clerks: Optional[Sequence[int]] = None,
                   check: bool = True):
-        """One round over every rank's participants; rank 0 gets the output."""
+        """One round over every rank's participants; rank 0 gets the output.
+
+        Every rank must hold the same number of participants (the routing
+        plan cuts each clerk's P boxes into fixed parts).
+        """
+        P = int(secrets_local.shape[0])
         return self.engine.run_round(secrets_local, clerks=clerks, check=check,
-                                     reducer=self._reduce, owner_base=_owner_base(self.rank))
+                                     reducer=self._reduce, owner_base=_owner_base(self.rank),
+                                     router=self.router(P))

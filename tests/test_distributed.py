@@ -43,7 +43,7 @@ def _inputs(rank, P, D, m):
     return rng.integers(0, m, size=(P, D), dtype=np.int64)
 
 
-def _worker(rank, world, port, name, P, D, clerks, q):
+def _worker(rank, world, port, name, P, D, clerks, layout, q):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -53,7 +53,7 @@ def _worker(rank, world, port, name, P, D, clerks, q):
         from sda_amd.parallel import DistributedAggregator
 
         spec = _spec(name, D)
-        agg = DistributedAggregator(spec, engine="host")
+        agg = DistributedAggregator(spec, engine="host", layout=layout)
         res = agg.run_round(_inputs(rank, P, D, spec.field_modulus), clerks=clerks)
         if rank == 0:
             expect = sum(_inputs(r, P, D, spec.field_modulus).sum(0) for r in range(world))
@@ -66,11 +66,11 @@ def _worker(rank, world, port, name, P, D, clerks, q):
         q.put(("err", f"rank {rank}: {type(e).__name__}: {e}"))
 
 
-def _run(world, name, P=3, D=17, clerks=None):
+def _run(world, name, P=3, D=17, clerks=None, layout="committee"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, P, D, clerks, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, P, D, clerks, layout, q))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -82,13 +82,20 @@ def _run(world, name, P=3, D=17, clerks=None):
     assert all(r[1] for r in results), results
 
 
+@pytest.mark.parametrize("layout", ["committee", "owner"])
 @pytest.mark.parametrize("name", ["additive", "fullmask", "chachamask", "pss", "bigmod"])
-def test_distributed_two_ranks(native, name):
-    _run(2, name)
+def test_distributed_two_ranks(native, name, layout):
+    _run(2, name, layout=layout)
 
 
-def test_distributed_three_ranks_pss_dropout(native):
-    _run(3, "pss5of8", P=2, D=10, clerks=[0, 2, 3, 5, 7])
+@pytest.mark.parametrize("layout", ["committee", "owner"])
+def test_distributed_three_ranks_pss_dropout(native, layout):
+    _run(3, "pss5of8", P=2, D=10, clerks=[0, 2, 3, 5, 7], layout=layout)
+
+
+def test_distributed_four_ranks_committee_spread(native):
+    # N - 1 >= n: boxes split over every peer, one clerk per (source, destination)
+    _run(4, "fullmask", P=5, D=9)
 
 
 def test_host_engine_single_process(native):

@@ -18,7 +18,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, name, q):
+def _worker(rank, world, port, name, layout, q):
     import torch
     import torch.distributed as dist
 
@@ -31,9 +31,11 @@ def _worker(rank, world, port, name, q):
         from sda_amd.parallel import DistributedAggregator
 
         D, P, m = 5000, 6, 433
-        spec = (AggregationSpec(D, m, Additive(3, m), FullMask(m)) if name == "fullmask"
-                else AggregationSpec(D, m, PSS_4_8_3))
-        agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", 0))
+        spec = {"fullmask": AggregationSpec(D, m, Additive(3, m), FullMask(m)),
+                "additive2": AggregationSpec(D, m, Additive(2, m)),
+                "pss": AggregationSpec(D, m, PSS_4_8_3)}[name]
+        agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", 0),
+                                    layout=layout)
 
         def inputs(r):
             g = torch.Generator().manual_seed(99 + r)
@@ -50,15 +52,19 @@ def _worker(rank, world, port, name, q):
         q.put(("err", f"rank {rank}: {type(e).__name__}: {e}"))
 
 
-@pytest.mark.parametrize("name", ["fullmask", "pss"])
-def test_distributed_device_two_ranks_one_gpu(cuda, name):
+@pytest.mark.parametrize("world,name,layout", [(2, "fullmask", "committee"),
+                                               (2, "pss", "committee"),
+                                               (2, "fullmask", "owner"),
+                                               (3, "additive2", "committee")])
+def test_distributed_device_ranks_one_gpu(cuda, world, name, layout):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, layout, q))
+             for r in range(world)]
     for p in procs:
         p.start()
-    results = [q.get(timeout=300) for _ in range(2)]
+    results = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
     errs = [r[1] for r in results if r[0] == "err"]
