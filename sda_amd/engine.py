@@ -137,26 +137,61 @@ class DeviceAggregator:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
+    def _live(self, clerks):
+        spec, n = self.spec, self.n
+        live = list(range(n)) if clerks is None else sorted(set(int(c) for c in clerks))
+        if self._pss is None and len(live) != n:
+            raise AggregationError("additive sharing needs every clerk's result")
+        if self._pss is not None and len(live) < spec.sharing.reconstruction_threshold():
+            raise AggregationError("Not enough shares to reconstruct")
+        return live
+
+    def new_error_word(self) -> torch.Tensor:
+        return torch.zeros(1, dtype=torch.int32, device=self.device)
+
     def run_round(self, secrets: torch.Tensor, clerks: Sequence[int] | None = None,
                   check: bool = True, reducer=None, owner_base: int = 0,
                   router=None) -> RoundResult:
         """One full round for participant vectors `secrets` [P][D] (int32, on device).
 
-        Stream schedule: every X25519 / key-derivation kernel (participants'
-        ephemeral keys, clerks' and recipient's key agreement) runs on a side
-        stream concurrently with the bandwidth-bound share/encode/MAC kernels of
-        the main stream; the main stream waits on events only where it consumes
-        derived keys.
+        = :meth:`participate_and_clerk` (+ `reducer`) + :meth:`reveal`.
 
         `reducer(partials) -> reduced | None` (multi-GPU): called with the
         per-clerk column sums over this device's participants -- int64
-        [len(live) (+1 with a mask)][B or D] -- before the recipient stage; it
-        returns the sums over all devices on the root and None elsewhere (which
-        then skips the recipient stage and returns ``output=None``).
+        [len(live) (+1 with a mask)][max(B, D)] -- before the recipient stage;
+        it returns the sums over all devices on the root and None elsewhere
+        (which then skips the recipient stage and returns ``output=None``).
         `owner_base` offsets the participants' RNG stream ids.
         `router.exchange(arena) -> inbox` (multi-GPU committee layout): moves
         the sealed clerk boxes to the ranks that play the clerks; the clerk
         stage then opens the inbox (same [n][P] clerk-major shape).
+        """
+        live = self._live(clerks)
+        err = self.new_error_word()
+        marks: list = []
+        self._mark(marks, "start")
+        combined, mask_sum = self.participate_and_clerk(secrets, live, err, owner_base=owner_base,
+                                                        router=router, marks=marks)
+        if reducer is not None:
+            combined, mask_sum = self.reduce_partials(combined, mask_sum, reducer, marks)
+            if combined is None:
+                return self._finish(err, marks, check, RoundResult(None, live, {}))
+        out = self.reveal(combined, mask_sum, live, err, marks=marks)
+        return self._finish(err, marks, check, RoundResult(out, live, {}))
+
+    def participate_and_clerk(self, secrets: torch.Tensor, live, err, owner_base: int = 0,
+                              router=None, marks=None):
+        """Participants mask + share + seal; clerks open + combine.
+
+        Returns (combined [len(live)][B] int32 in [0, m), mask_sum [D] int32 or
+        None): the clerks' sums over these participants and the recipient's
+        sum of their masks. A fresh 256-bit round key is drawn per call, so
+        ephemeral keys and share streams never repeat across calls (waves).
+
+        Stream schedule: every X25519 / key-derivation kernel (participants'
+        ephemeral keys, clerks' key agreement) runs on a side stream concurrently
+        with the bandwidth-bound share/encode/MAC kernels of the main stream;
+        the main stream waits on events only where it consumes derived keys.
         """
         spec, n, m = self.spec, self.n, self.m
         if secrets.dim() != 2 or secrets.shape[1] != spec.dimension:
@@ -166,50 +201,39 @@ class DeviceAggregator:
         secrets = secrets.contiguous()
         P, D = secrets.shape
         B = spec.batches
-        live = list(range(n)) if clerks is None else sorted(set(int(c) for c in clerks))
-        if self._pss is None and len(live) != n:
-            raise AggregationError("additive sharing needs every clerk's result")
-        if self._pss is not None and len(live) < spec.sharing.reconstruction_threshold():
-            raise AggregationError("Not enough shares to reconstruct")
+        marks = [] if marks is None else marks
         dev = self.device
         rng_key = native().crypto.random_bytes(32)
         self._round += 1
-        err = torch.zeros(1, dtype=torch.int32, device=dev)
-        marks: list = []
-        self._mark(marks, "start")
         main = torch.cuda.current_stream(dev)
         side = self._side_stream()
-        pks, sks = self.keys.pks, self.keys.sks
+        pks = self.keys.pks
 
-        # ---- arenas (participants -> clerks, participants -> recipient, clerks -> recipient)
+        # ---- arenas (participants -> clerks, participants -> recipient)
         clerk_arena = Arena.empty(n * P, B, m, dev)
         mask_arena = None
         if isinstance(spec.masking, FullMask):
             mask_arena = Arena.empty(P, D, m, dev)
         elif isinstance(spec.masking, ChaChaMask):
             mask_arena = Arena.empty(P, spec.masking.seed_words, 0, dev)
-        res_arena = Arena.empty(len(live), B, m, dev)
-        kidx_clerk = torch.arange(n, dtype=torch.int32, device=dev).repeat_interleave(P)
+        kidx_clerk = self._kidx_clerk(P)
         kidx_rcpt_p = torch.full((P,), n, dtype=torch.int32, device=dev)
-        kidx_rcpt_c = torch.full((len(live),), n, dtype=torch.int32, device=dev)
 
-        # ---- side stream: all key agreement (data independent)
+        # ---- side stream: key agreement (data independent)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             ks_clerk = seal_setup(clerk_arena, kidx_clerk, pks, rng_key, 0, err)
             ks_mask = (seal_setup(mask_arena, kidx_rcpt_p, pks, rng_key, n * P, err)
                        if mask_arena is not None else None)
-            ks_res = seal_setup(res_arena, kidx_rcpt_c, pks, rng_key, (n + 1) * P, err)
             ev_sealkeys = torch.cuda.Event()
             ev_sealkeys.record(side)
             ko_clerk = self._open_keys(clerk_arena, kidx_clerk, live, P, err) \
                 if router is None else []
-            ko_res = open_setup(res_arena, kidx_rcpt_c, sks, pks, err)
-            ko_mask = (open_setup(mask_arena, kidx_rcpt_p, sks, pks, err)
+            ko_mask = (open_setup(mask_arena, kidx_rcpt_p, self.keys.sks, pks, err)
                        if mask_arena is not None else None)
             ev_openkeys = torch.cuda.Event()
             ev_openkeys.record(side)
-        for t in [ks_clerk, ks_mask, ks_res, ko_res, ko_mask] + ko_clerk:
+        for t in [ks_clerk, ks_mask, ko_mask] + ko_clerk:
             if t is not None:
                 t.record_stream(main)
 
@@ -217,6 +241,7 @@ class DeviceAggregator:
         shares, cnt, mask_vals, mask_cnt = self._share(secrets, rng_key, owner_base, err)
         main.wait_event(ev_sealkeys)
         seal_data(clerk_arena, ks_clerk, shares.view(n * P, B), err, cnt)
+        del shares
         if mask_arena is not None:
             seal_data(mask_arena, ks_mask, mask_vals, err, mask_cnt)
         self._mark(marks, "participate")
@@ -227,6 +252,7 @@ class DeviceAggregator:
         if router is not None:
             # snapshot transpose over xGMI: boxes travel to the clerks' ranks
             inbox = router.exchange(clerk_arena)
+            del clerk_arena
             self._mark(marks, "exchange")
             ko_clerk = self._open_keys(inbox, kidx_clerk, live, P, err)
         if len(live) == n:
@@ -235,10 +261,12 @@ class DeviceAggregator:
             vals = torch.empty(len(live), P, B, dtype=self.vdtype, device=dev)
             for i, c in enumerate(live):
                 open_data(inbox.slice(c * P, P), ko_clerk[i], err, out=vals[i])
+        del inbox
         combined = torch.empty(len(live), B, dtype=torch.int32, device=dev)
         G.colsum(vals.view(len(live), P, B), m, combined)
-        # recipient's share of the mask work is data-parallel too: open this
-        # device's participants' mask boxes and sum them
+        del vals
+        # recipient's share of the mask work is data-parallel too: open these
+        # participants' mask boxes and sum them
         mask_sum = None
         if mask_arena is not None:
             mask_sum = torch.empty(D, dtype=torch.int32, device=dev)
@@ -248,28 +276,42 @@ class DeviceAggregator:
             else:
                 G.chacha_mask_sum(mvals, D, m, mask_sum, err)
         self._mark(marks, "clerk")
+        return combined, mask_sum
 
-        if reducer is not None:
-            # one bucket: clerk sums (B wide) and the mask sum (D wide) as rows
-            nrow = len(live) + (1 if mask_sum is not None else 0)
-            partials = torch.zeros(nrow, max(B, D), dtype=torch.int64, device=dev)
-            partials[:len(live), :B] = combined
-            if mask_sum is not None:
-                partials[len(live), :D] = mask_sum
-            reduced = reducer(partials)
+    def reduce_partials(self, combined, mask_sum, reducer, marks=None):
+        """Bucket the clerk rows (B wide) and the mask row (D wide) into one
+        int64 buffer, reduce over devices, unpack on the root."""
+        B, D, m = self.spec.batches, self.spec.dimension, self.m
+        rows = combined.shape[0]
+        nrow = rows + (1 if mask_sum is not None else 0)
+        partials = torch.zeros(nrow, max(B, D), dtype=torch.int64, device=self.device)
+        partials[:rows, :B] = combined
+        if mask_sum is not None:
+            partials[rows, :D] = mask_sum
+        reduced = reducer(partials)
+        if marks is not None:
             self._mark(marks, "reduce")
-            if reduced is None:
-                return self._finish(err, marks, check, RoundResult(None, live, {}))
-            reduced = torch.remainder(reduced, m).to(torch.int32)
-            combined = reduced[:len(live), :B].contiguous()
-            if mask_sum is not None:
-                mask_sum = reduced[len(live), :D].contiguous()
+        if reduced is None:
+            return None, None
+        reduced = torch.remainder(reduced, m).to(torch.int32)
+        combined = reduced[:rows, :B].contiguous()
+        if mask_sum is not None:
+            mask_sum = reduced[rows, :D].contiguous()
+        return combined, mask_sum
 
-        # ---- clerks reseal their results for the recipient
+    def reveal(self, combined, mask_sum, live, err, marks=None) -> torch.Tensor:
+        """Clerks seal their sums for the recipient; the recipient opens them,
+        reconstructs (sum / Lagrange over the live clerks) and unmasks."""
+        spec, n, m = self.spec, self.n, self.m
+        B, D, dev = spec.batches, spec.dimension, self.device
+        pks, sks = self.keys.pks, self.keys.sks
+        rng_key = native().crypto.random_bytes(32)
+        res_arena = Arena.empty(len(live), B, m, dev)
+        kidx_rcpt_c = torch.full((len(live),), n, dtype=torch.int32, device=dev)
+        ks_res = seal_setup(res_arena, kidx_rcpt_c, pks, rng_key, 0, err)
         res_vals = combined if self.vdtype == torch.int32 else combined.to(self.vdtype)
         seal_data(res_arena, ks_res, res_vals, err)
-
-        # ---- recipient: open results, reconstruct, unmask
+        ko_res = open_setup(res_arena, kidx_rcpt_c, sks, pks, err)
         ys = open_data(res_arena, ko_res, err, out_dtype=torch.int32)
         masked = torch.empty(D, dtype=torch.int32, device=dev)
         if self._pss is None:
@@ -281,8 +323,18 @@ class DeviceAggregator:
         if mask_sum is not None:
             out = torch.empty(D, dtype=torch.int32, device=dev)
             G.sub_mod(masked, mask_sum, m, out)
-        self._mark(marks, "reveal")
-        return self._finish(err, marks, check, RoundResult(out, live, {}))
+        if marks is not None:
+            self._mark(marks, "reveal")
+        return out
+
+    def _kidx_clerk(self, P: int) -> torch.Tensor:
+        cache = getattr(self, "_kidx_cache", None)
+        if cache is None:
+            cache = self._kidx_cache = {}
+        if P not in cache:
+            cache[P] = torch.arange(self.n, dtype=torch.int32,
+                                    device=self.device).repeat_interleave(P)
+        return cache[P]
 
     def _open_keys(self, arena, kidx, live, P, err):
         pks, sks = self.keys.pks, self.keys.sks

@@ -131,3 +131,22 @@ class DistributedAggregator:
         return self.engine.run_round(secrets_local, clerks=clerks, check=check,
                                      reducer=self._reduce, owner_base=_owner_base(self.rank),
                                      router=self.router(P))
+
+    def run_streamed(self, total_local: int, make_wave, wave: int = 64,
+                     clerks: Optional[Sequence[int]] = None, checkpoint: Optional[str] = None,
+                     checkpoint_every: int = 8, resume: bool = True):
+        """Stream this rank's `total_local` participants in waves (device engine).
+
+        Every rank must stream the same number of participants with the same
+        wave size (the routing plan is per wave size). Checkpoints are per
+        rank: pass a rank-specific path.
+        """
+        if self.kind != "device":
+            raise ValueError("streaming runs on the device engine")
+        from ..streaming import StreamingAggregator
+
+        st = StreamingAggregator(self.engine, wave=wave, checkpoint=checkpoint,
+                                 checkpoint_every=checkpoint_every)
+        return st.run(total_local, make_wave, clerks=clerks, reducer=self._reduce,
+                      router_for=self.router if self.layout == "committee" else None,
+                      owner_base=_owner_base(self.rank), resume=resume)
