@@ -122,4 +122,19 @@ void launch_pss_reconstruct(int B, int k, int nI, int D, uint32_t p, const uint3
 void launch_sub_mod(int D, uint32_t m, const uint32_t* a, const uint32_t* b, uint32_t* out,
                     hipStream_t s);
 
+// ---- modgemm.hip -----------------------------------------------------------
+// C = A . B mod p (p < 2^28) on i8 MFMA with `limbs` (3 or 4) 7-bit limbs. A limbs
+// [L][M][Kp], B limbs [L][batches][N][Kp] (b_plane = batches*N*Kp bytes between limb
+// planes), C[z*ldc_z + m*ldc_m + n*ldc_n] written where that index < limit.
+void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p, const int8_t* A,
+                       const int8_t* B, int64_t b_plane, int value_bytes, void* C, int64_t ldc_z,
+                       int64_t ldc_m, int64_t ldc_n, int64_t limit, hipStream_t s);
+// X limbs [3][P][B][Kp] of packed-Shamir inputs: secrets (canonical) then t draws.
+void launch_pss_x_limbs(int P, int D, int B, int k, int t, int Kp, int limbs, uint32_t p,
+                        const int32_t* secrets, RngKeyArg rng, uint64_t owner_base, int8_t* X,
+                        hipStream_t s);
+// Limbs of Y [R][N] transposed to [3][N][Kp].
+void launch_limbs_t(int R, int N, int Kp, int limbs, const uint32_t* Y, int8_t* out,
+                    hipStream_t s);
+
 }  // namespace sdagpu

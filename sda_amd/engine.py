@@ -70,7 +70,7 @@ class DeviceAggregator:
     """Runs complete aggregation rounds for one :class:`AggregationSpec`."""
 
     def __init__(self, spec: AggregationSpec, device=None, keys: KeyTable | None = None,
-                 time_stages: bool = False):
+                 time_stages: bool = False, pss_backend: str = "auto"):
         self.spec = spec
         self.device = torch.device(device or "cuda")
         self.n = spec.n_clerks
@@ -85,8 +85,21 @@ class DeviceAggregator:
             self._pss = p
             self._share_matrix = torch.tensor(p.share_matrix(), dtype=torch.int64).to(
                 torch.int32).to(self.device)
+            ps = spec.sharing
+            big = ps.secret_count > 8 or ps.privacy_threshold_ > 16 or ps.share_count > 64
+            if pss_backend not in ("auto", "mfma", "valu"):
+                raise ValueError("pss_backend must be auto, mfma or valu")
+            if pss_backend == "valu" and big:
+                raise ValueError("the register (VALU) PSS kernel supports k<=8, t<=16, n<=64")
+            # matrix cores (int8-limb MFMA GEMM) for the large parameter sets
+            self._pss_mfma = pss_backend == "mfma" or (pss_backend == "auto" and big)
+            if self._pss_mfma:
+                self._limbs = G.limb_count(self.m)
+                self._Kp = G.padded_k(ps.secret_count + ps.privacy_threshold_)
+                self._M_limbs = G.limbs_of(self._share_matrix, self._Kp, self._limbs)
         else:
             self._pss = None
+            self._pss_mfma = False
 
     # ------------------------------------------------------------ helpers ----
     def _key_idx(self, values: Sequence[int]) -> torch.Tensor:
@@ -116,6 +129,20 @@ class DeviceAggregator:
             mask_mode = G.MASK_CHACHA
             seed_words = spec.masking.seed_words
             mask_vals = torch.empty(P, seed_words, dtype=torch.int32, device=dev)
+        if self._pss_mfma:
+            # masks (if any) first, then S = M . X on the matrix cores
+            masked = secrets
+            if mask_mode != G.MASK_NONE:
+                masked = G.mask_secrets(secrets, m, mask_mode, rng_key, owner_base,
+                                        mask_out=mask_vals if mask_mode == G.MASK_FULL else None,
+                                        mask_cnt=mask_cnt,
+                                        seeds=mask_vals if mask_mode == G.MASK_CHACHA else None,
+                                        seed_words=seed_words, err=err)
+            ps = spec.sharing
+            X = G.pss_x_limbs(masked, ps.secret_count, ps.privacy_threshold_, m, rng_key, owner_base)
+            G.modgemm_i8(self._M_limbs, X, m, shares, ldc_z=B, ldc_m=P * B, ldc_n=1,
+                         limit=n * P * B)
+            return shares, None, mask_vals, mask_cnt
         if self._pss is None:
             G.share_additive(secrets, n, m, shares, cnt, mask_mode, rng_key, owner_base,
                              mask_out=mask_vals if mask_mode == G.MASK_FULL else None,
@@ -170,13 +197,14 @@ class DeviceAggregator:
         err = self.new_error_word()
         marks: list = []
         self._mark(marks, "start")
+        rk = self.prepare_reveal(live, err)
         combined, mask_sum = self.participate_and_clerk(secrets, live, err, owner_base=owner_base,
                                                         router=router, marks=marks)
         if reducer is not None:
             combined, mask_sum = self.reduce_partials(combined, mask_sum, reducer, marks)
             if combined is None:
                 return self._finish(err, marks, check, RoundResult(None, live, {}))
-        out = self.reveal(combined, mask_sum, live, err, marks=marks)
+        out = self.reveal(combined, mask_sum, live, err, marks=marks, keys=rk)
         return self._finish(err, marks, check, RoundResult(out, live, {}))
 
     def participate_and_clerk(self, secrets: torch.Tensor, live, err, owner_base: int = 0,
@@ -299,23 +327,46 @@ class DeviceAggregator:
             mask_sum = reduced[rows, :D].contiguous()
         return combined, mask_sum
 
-    def reveal(self, combined, mask_sum, live, err, marks=None) -> torch.Tensor:
+    def prepare_reveal(self, live, err):
+        """Key agreement for the clerks -> recipient boxes, on the side stream
+        (latency-bound X25519 ladders for a handful of messages: kept off the
+        critical path). Returns what :meth:`reveal` consumes."""
+        n, m, dev = self.n, self.m, self.device
+        pks, sks = self.keys.pks, self.keys.sks
+        rng_key = native().crypto.random_bytes(32)
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream()
+        res_arena = Arena.empty(len(live), self.spec.batches, m, dev)
+        kidx = torch.full((len(live),), n, dtype=torch.int32, device=dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            ks = seal_setup(res_arena, kidx, pks, rng_key, 0, err)
+            ko = open_setup(res_arena, kidx, sks, pks, err)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        for t in (res_arena.ct, res_arena.pt_len, kidx):  # main-stream tensors used on side
+            t.record_stream(side)
+        for t in (ks, ko):  # side-stream tensors consumed on main
+            t.record_stream(main)
+        return res_arena, ks, ko, ev
+
+    def reveal(self, combined, mask_sum, live, err, marks=None, keys=None) -> torch.Tensor:
         """Clerks seal their sums for the recipient; the recipient opens them,
         reconstructs (sum / Lagrange over the live clerks) and unmasks."""
         spec, n, m = self.spec, self.n, self.m
         B, D, dev = spec.batches, spec.dimension, self.device
-        pks, sks = self.keys.pks, self.keys.sks
-        rng_key = native().crypto.random_bytes(32)
-        res_arena = Arena.empty(len(live), B, m, dev)
-        kidx_rcpt_c = torch.full((len(live),), n, dtype=torch.int32, device=dev)
-        ks_res = seal_setup(res_arena, kidx_rcpt_c, pks, rng_key, 0, err)
+        res_arena, ks_res, ko_res, ev = keys if keys is not None else self.prepare_reveal(live, err)
+        torch.cuda.current_stream(dev).wait_event(ev)
         res_vals = combined if self.vdtype == torch.int32 else combined.to(self.vdtype)
         seal_data(res_arena, ks_res, res_vals, err)
-        ko_res = open_setup(res_arena, kidx_rcpt_c, sks, pks, err)
         ys = open_data(res_arena, ko_res, err, out_dtype=torch.int32)
         masked = torch.empty(D, dtype=torch.int32, device=dev)
         if self._pss is None:
             G.colsum(ys.view(1, n, B), m, masked)
+        elif self._pss_mfma:
+            lag_limbs, kp = self._lagrange_limbs(live)
+            G.modgemm_i8(lag_limbs, G.limbs_t(ys, kp, self._limbs), m, masked, ldc_z=0, ldc_m=1,
+                         ldc_n=spec.sharing.secret_count, limit=D)
         else:
             lag = self._lagrange(live)
             G.pss_reconstruct(ys, lag, spec.sharing.secret_count, D, m, masked)
@@ -351,6 +402,16 @@ class DeviceAggregator:
             for (a, ea), (b, eb) in zip(marks, marks[1:]):
                 result.stage_ms[b] = ea.elapsed_time(eb)
         return result
+
+    def _lagrange_limbs(self, live):
+        key = ("limbs",) + tuple(live)
+        cache = getattr(self, "_lag_cache", None)
+        if cache is None:
+            cache = self._lag_cache = {}
+        if key not in cache:
+            kp = G.padded_k(len(live))
+            cache[key] = (G.limbs_of(self._lagrange(live), kp, self._limbs), kp)
+        return cache[key]
 
     def _lagrange(self, live):
         key = tuple(live)

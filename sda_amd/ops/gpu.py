@@ -138,6 +138,29 @@ def share_additive(secrets, n, modulus, shares, cnt, mask_mode, rng_key, owner_b
                           _ptr(seeds) if seeds is not None else z, _ptr(err), _stream())
 
 
+def mask_secrets(secrets, modulus, mask_mode, rng_key, owner_base, mask_out=None, mask_cnt=None,
+                 seeds=None, seed_words=0, err=None) -> torch.Tensor:
+    """Masked secrets (canonical int32 [P][D]) + mask outputs: the additive
+    share kernel with a single share, whose only share is the masked secret."""
+    P, D = secrets.shape
+    _check(secrets, "secrets", torch.int32)
+    _check(err, "err", torch.int32, numel=1)
+    if mask_mode == MASK_FULL:
+        _check(mask_out, "mask_out", torch.int32, numel=P * D)
+        _check(mask_cnt, "mask_cnt", torch.int32, numel=P * tiles(D))
+    if mask_mode == MASK_CHACHA:
+        _check(seeds, "seeds", torch.int32, numel=P * seed_words)
+    masked = torch.empty(P, D, dtype=torch.int32, device=secrets.device)
+    cnt = torch.empty(P * tiles(D), dtype=torch.int32, device=secrets.device)
+    z = 0
+    _gpu().share_additive(P, D, 1, modulus, 4, _ptr(secrets), mask_mode, seed_words,
+                          rng_words(rng_key), owner_base, _ptr(masked), _ptr(cnt),
+                          _ptr(mask_out) if mask_out is not None else z,
+                          _ptr(mask_cnt) if mask_cnt is not None else z,
+                          _ptr(seeds) if seeds is not None else z, _ptr(err), _stream())
+    return masked
+
+
 def share_pss(secrets, n, k, t, prime, matrix, shares, cnt, mask_mode, rng_key, owner_base,
               mask_out=None, seeds=None, seed_words=0, err=None):
     P, D = secrets.shape
@@ -243,3 +266,66 @@ def sub_mod(a: torch.Tensor, b: torch.Tensor, modulus: int, out: torch.Tensor):
     _check(b, "b", torch.int32, numel=a.numel())
     _check(out, "out", torch.int32, numel=a.numel())
     _gpu().sub_mod(a.numel(), modulus, _ptr(a), _ptr(b), _ptr(out), _stream())
+
+
+# ---- packed Shamir on the matrix cores (int8 limbs; modgemm.hip) ----------------
+def padded_k(K: int) -> int:
+    return (K + 63) // 64 * 64
+
+
+def limb_count(prime: int) -> int:
+    """7-bit limbs per element: 3 for p < 2^21, 4 for p < 2^28."""
+    if prime < 2 ** 21:
+        return 3
+    if prime < 2 ** 28:
+        return 4
+    raise ValueError("modgemm: modulus must be < 2^28")
+
+
+def limbs_of(values: torch.Tensor, Kp: int, limbs: int) -> torch.Tensor:
+    """Limb planes [L][rows][Kp] (int8) of a [rows][K] matrix of field elements."""
+    rows, K = values.shape
+    v = values.to(torch.int64)
+    out = torch.zeros(limbs, rows, Kp, dtype=torch.int8, device=values.device)
+    for l in range(limbs):
+        out[l, :, :K] = ((v >> (7 * l)) & 0x7F).to(torch.int8)
+    return out
+
+
+def modgemm_i8(A_limbs: torch.Tensor, B_limbs: torch.Tensor, prime: int, out: torch.Tensor,
+               ldc_z: int, ldc_m: int, ldc_n: int, limit: int):
+    """out[z*ldc_z + m*ldc_m + n*ldc_n] = (A . B_z)[m][n] mod prime (A [L][M][Kp], B [L][Z][N][Kp])."""
+    _check(A_limbs, "A_limbs", torch.int8)
+    _check(B_limbs, "B_limbs", torch.int8)
+    L, M, Kp = A_limbs.shape
+    Lb, Z, N, Kb = B_limbs.shape
+    if Kb != Kp or Lb != L or L != limb_count(prime):
+        raise ValueError("limb shape mismatch")
+    vb = value_bytes(out.dtype)
+    max_idx = (Z - 1) * ldc_z + (M - 1) * ldc_m + (N - 1) * ldc_n
+    if min(limit, max_idx + 1) > out.numel():
+        raise ValueError("output too small for the GEMM index map")
+    _gpu().modgemm_i8(M, N, Kp, Z, L, prime, _ptr(A_limbs), _ptr(B_limbs), Z * N * Kp, vb,
+                      _ptr(out), ldc_z, ldc_m, ldc_n, limit, _stream())
+
+
+def pss_x_limbs(secrets: torch.Tensor, k: int, t: int, prime: int, rng_key: bytes,
+                owner_base: int) -> torch.Tensor:
+    P, D = secrets.shape
+    _check(secrets, "secrets", torch.int32)
+    B = (D + k - 1) // k
+    Kp = padded_k(k + t)
+    L = limb_count(prime)
+    X = torch.empty(L, P, B, Kp, dtype=torch.int8, device=secrets.device)
+    _gpu().pss_x_limbs(P, D, B, k, t, Kp, L, prime, _ptr(secrets), rng_words(rng_key), owner_base,
+                       _ptr(X), _stream())
+    return X
+
+
+def limbs_t(Y: torch.Tensor, Kp: int, limbs: int) -> torch.Tensor:
+    """Limbs of Y [R][N] (int32 field elements) transposed to [L][1][N][Kp]."""
+    R, N = Y.shape
+    _check(Y, "Y", torch.int32)
+    out = torch.empty(limbs, 1, N, Kp, dtype=torch.int8, device=Y.device)
+    _gpu().limbs_t(R, N, Kp, limbs, _ptr(Y), _ptr(out), _stream())
+    return out

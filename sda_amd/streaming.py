@@ -106,6 +106,7 @@ class StreamingAggregator:
         err = eng.new_error_word()
         marks: list = []
         eng._mark(marks, "start")
+        rk = eng.prepare_reveal(live, err)
         done = 0
         for w in range(start, waves):
             first = w * self.wave
@@ -134,7 +135,7 @@ class StreamingAggregator:
             if combined is None:
                 self._check(err)
                 return StreamResult(None, live, done, start)
-        out = eng.reveal(combined, mask_sum, live, err, marks=marks)
+        out = eng.reveal(combined, mask_sum, live, err, marks=marks, keys=rk)
         if check:
             self._check(err)
         res = StreamResult(out, live, done, start)
