@@ -88,6 +88,7 @@ PYBIND11_MODULE(_sda_gpu, m) {
            int seed_words, std::vector<uint32_t> rng, uint64_t owner_base, uintptr_t shares,
            uintptr_t cnt, uintptr_t mask_out, uintptr_t mask_cnt, uintptr_t seeds, uintptr_t err,
            uintptr_t stream) {
+          if (n < 1 || n > 256) throw std::invalid_argument("share_additive: n must be 1..256");
           launch_share_additive(Pn, D, n, mod, value_bytes, P<const int32_t>(secrets), mask_mode,
                                 seed_words, rng_from(rng), owner_base, P<void>(shares),
                                 P<uint32_t>(cnt), P<uint32_t>(mask_out), P<uint32_t>(mask_cnt),

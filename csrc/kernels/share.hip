@@ -405,7 +405,7 @@ void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, con
                            void* shares, uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt,
                            uint32_t* seeds, uint32_t* err, hipStream_t s) {
   if (P <= 0 || D <= 0) return;
-  if (n < 2 || n > kMaxCountSlots) return;  // validated on the Python side
+  if (n < 1 || n > kMaxCountSlots) return;  // rejected by the binding (n == 1: masking only)
   ModParams mp = make_mod_params(m);
   if (mask_mode == kMaskChaCha)
     hipLaunchKernelGGL(k_chacha_seeds, dim3((P + 63) / 64), dim3(64), 0, s, P, seed_words, rng,

@@ -96,7 +96,9 @@ class DeviceAggregator:
             if self._pss_mfma:
                 self._limbs = G.limb_count(self.m)
                 self._Kp = G.padded_k(ps.secret_count + ps.privacy_threshold_)
-                self._M_limbs = G.limbs_of(self._share_matrix, self._Kp, self._limbs)
+                self._M_limbs = G.limbs_of(
+                    self._share_matrix.view(self.n, ps.secret_count + ps.privacy_threshold_),
+                    self._Kp, self._limbs)
         else:
             self._pss = None
             self._pss_mfma = False
@@ -410,7 +412,8 @@ class DeviceAggregator:
             cache = self._lag_cache = {}
         if key not in cache:
             kp = G.padded_k(len(live))
-            cache[key] = (G.limbs_of(self._lagrange(live), kp, self._limbs), kp)
+            lag = self._lagrange(live).view(self.spec.sharing.secret_count, len(live))
+            cache[key] = (G.limbs_of(lag, kp, self._limbs), kp)
         return cache[key]
 
     def _lagrange(self, live):
