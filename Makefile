@@ -40,9 +40,9 @@ HIP_BIND := csrc/kernels/gpu_module.cpp
 
 NATIVE_MOD := $(LIB)/_sda_native$(EXT)
 GPU_MOD    := $(LIB)/_sda_gpu$(EXT)
-BINS       := $(patsubst csrc/bin/%.cc,$(BIN)/%,$(filter-out csrc/bin/sda_selftest.cc,$(wildcard csrc/bin/*.cc)))
+BINS       := $(patsubst csrc/bin/%.cc,$(BIN)/%,$(wildcard csrc/bin/*.cc))
 
-.PHONY: all host gpu clean asan
+.PHONY: all host gpu clean asan tsan selftest emul
 all: host gpu
 host: $(NATIVE_MOD) $(BINS)
 gpu: $(GPU_MOD)
@@ -79,11 +79,22 @@ $(GPU_MOD): $(HIP_OBJ) $(BUILD)/hip/gpu_module.o $(CORE_LIB)
 	@mkdir -p $(dir $@)
 	$(HIPCC) -shared --offload-arch=$(GPU_ARCH) -o $@ $^ -pthread
 
-asan:
-	@mkdir -p $(BUILD)/asan
-	$(CXX) -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer $(INCS) \
-	    csrc/bin/sda_selftest.cc $(CORE_SRC) -o $(BUILD)/asan/sda_selftest -pthread
+# sanitizer builds of the host control plane; run the C++ self-test
+asan: $(BUILD)/asan/sda_selftest
 	$(BUILD)/asan/sda_selftest
+$(BUILD)/asan/sda_selftest: csrc/bin/sda_selftest.cc $(CORE_SRC) $(wildcard csrc/include/sda/*.hpp)
+	@mkdir -p $(BUILD)/asan
+	$(CXX) -O1 -g -std=c++17 -fsanitize=address,undefined -fno-sanitize-recover=undefined \
+	    -fno-omit-frame-pointer $(INCS) csrc/bin/sda_selftest.cc $(CORE_SRC) \
+	    -o $@ -pthread
+tsan: $(BUILD)/tsan/sda_selftest
+	TSAN_OPTIONS=halt_on_error=1 $(BUILD)/tsan/sda_selftest
+$(BUILD)/tsan/sda_selftest: csrc/bin/sda_selftest.cc $(CORE_SRC) $(wildcard csrc/include/sda/*.hpp)
+	@mkdir -p $(BUILD)/tsan
+	$(CXX) -O1 -g -std=c++17 -fsanitize=thread -fno-omit-frame-pointer $(INCS) \
+	    csrc/bin/sda_selftest.cc $(CORE_SRC) -o $@ -pthread
+selftest: $(BIN)/sda_selftest
+	$(BIN)/sda_selftest
 
 clean:
 	rm -rf $(BUILD) $(LIB)/*.so $(BIN)
