@@ -29,6 +29,9 @@ from ._native import native
 from .models.schemes import Additive, AggregationSpec, ChaChaMask, FullMask, PackedShamir
 from .ops import gpu as G
 from .ops.sealed import Arena, open_, open_data, open_setup, seal, seal_data, seal_setup
+from .utils.trace import tracing_enabled
+
+_TRACE = tracing_enabled()
 
 
 class AggregationError(RuntimeError):
@@ -108,6 +111,10 @@ class DeviceAggregator:
         return torch.tensor(list(values), dtype=torch.int32, device=self.device)
 
     def _mark(self, marks, name):
+        # stage boundary: a roctx marker under SDA_TRACE=1 (rocprofv3 --marker-trace),
+        # a timing event with time_stages
+        if _TRACE:
+            torch.cuda.nvtx.mark(f"sda:{name}")
         if self.time_stages:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
