@@ -187,7 +187,7 @@ class DeviceAggregator:
 
     def run_round(self, secrets: torch.Tensor, clerks: Sequence[int] | None = None,
                   check: bool = True, reducer=None, owner_base: int = 0,
-                  router=None) -> RoundResult:
+                  router=None, router_for=None, waves: int = 1) -> RoundResult:
         """One full round for participant vectors `secrets` [P][D] (int32, on device).
 
         = :meth:`participate_and_clerk` (+ `reducer`) + :meth:`reveal`.
@@ -200,15 +200,25 @@ class DeviceAggregator:
         `owner_base` offsets the participants' RNG stream ids.
         `router.exchange(arena) -> inbox` (multi-GPU committee layout): moves
         the sealed clerk boxes to the ranks that play the clerks; the clerk
-        stage then opens the inbox (same [n][P] clerk-major shape).
+        stage then opens the inbox (same [n][P] clerk-major shape). With
+        `router_for(P_wave)` and `waves > 1` the exchange is pipelined behind
+        the next wave's compute (:meth:`participate_and_clerk_pipelined`).
         """
         live = self._live(clerks)
         err = self.new_error_word()
         marks: list = []
         self._mark(marks, "start")
         rk = self.prepare_reveal(live, err)
-        combined, mask_sum = self.participate_and_clerk(secrets, live, err, owner_base=owner_base,
-                                                        router=router, marks=marks)
+        if router_for is not None and waves > 1:
+            self._mark(marks, "participate")
+            combined, mask_sum = self.participate_and_clerk_pipelined(
+                secrets, live, err, router_for, waves, owner_base=owner_base, marks=marks)
+        else:
+            if router is None and router_for is not None:
+                router = router_for(secrets.shape[0])
+            combined, mask_sum = self.participate_and_clerk(secrets, live, err,
+                                                            owner_base=owner_base, router=router,
+                                                            marks=marks)
         if reducer is not None:
             combined, mask_sum = self.reduce_partials(combined, mask_sum, reducer, marks)
             if combined is None:
@@ -230,6 +240,55 @@ class DeviceAggregator:
         with the bandwidth-bound share/encode/MAC kernels of the main stream;
         the main stream waits on events only where it consumes derived keys.
         """
+        marks = [] if marks is None else marks
+        st = self._participate(secrets, live, err, owner_base, local_clerks=router is None)
+        self._mark(marks, "participate")
+        if router is not None:
+            # snapshot transpose over xGMI: boxes travel to the clerks' ranks
+            st["inbox"] = router.exchange(st.pop("clerk_arena"))
+            self._mark(marks, "exchange")
+        out = self._clerk(st, live, err)
+        self._mark(marks, "clerk")
+        return out
+
+    def participate_and_clerk_pipelined(self, secrets: torch.Tensor, live, err, router_for,
+                                        waves: int, owner_base: int = 0, marks=None):
+        """Committee layout with the exchange hidden behind compute.
+
+        The participants are cut into `waves`; wave w's grouped send/recv runs
+        on the communicator stream while wave w+1 is masked, shared and sealed,
+        and wave w is opened once its transfer has landed. Same result as
+        :meth:`participate_and_clerk` with a router (sums over all waves).
+        """
+        marks = [] if marks is None else marks
+        P = secrets.shape[0]
+        bounds = [(P * w // waves, P * (w + 1) // waves) for w in range(waves)]
+        bounds = [(lo, hi) for lo, hi in bounds if hi > lo]
+        acc, macc, pending = None, None, None
+
+        def finish(st):
+            nonlocal acc, macc
+            st["handle"].wait()
+            comb, msum = self._clerk(st, live, err)
+            acc = comb if acc is None else acc + comb
+            if msum is not None:
+                macc = msum if macc is None else macc + msum
+
+        for lo, hi in bounds:
+            st = self._participate(secrets[lo:hi], live, err, owner_base + lo, local_clerks=False)
+            st["inbox"], st["handle"] = router_for(hi - lo).exchange_async(st["clerk_arena"])
+            if pending is not None:
+                finish(pending)
+            pending = st
+        finish(pending)
+        self._mark(marks, "clerk")
+        m = self.m
+        return (torch.remainder(acc, m) if len(bounds) > 1 else acc,
+                torch.remainder(macc, m) if (macc is not None and len(bounds) > 1) else macc)
+
+    def _participate(self, secrets, live, err, owner_base, local_clerks: bool):
+        """Mask + share + seal one batch of participants; returns the state the
+        clerk half needs (arenas and derived keys)."""
         spec, n, m = self.spec, self.n, self.m
         if secrets.dim() != 2 or secrets.shape[1] != spec.dimension:
             raise ValueError("secrets must be [P][dimension]")
@@ -238,7 +297,6 @@ class DeviceAggregator:
         secrets = secrets.contiguous()
         P, D = secrets.shape
         B = spec.batches
-        marks = [] if marks is None else marks
         dev = self.device
         rng_key = native().crypto.random_bytes(32)
         self._round += 1
@@ -265,12 +323,12 @@ class DeviceAggregator:
             ev_sealkeys = torch.cuda.Event()
             ev_sealkeys.record(side)
             ko_clerk = self._open_keys(clerk_arena, kidx_clerk, live, P, err) \
-                if router is None else []
+                if local_clerks else None
             ko_mask = (open_setup(mask_arena, kidx_rcpt_p, self.keys.sks, pks, err)
                        if mask_arena is not None else None)
             ev_openkeys = torch.cuda.Event()
             ev_openkeys.record(side)
-        for t in [ks_clerk, ks_mask, ko_mask] + ko_clerk:
+        for t in [ks_clerk, ks_mask, ko_mask] + (ko_clerk or []):
             if t is not None:
                 t.record_stream(main)
 
@@ -281,17 +339,22 @@ class DeviceAggregator:
         del shares
         if mask_arena is not None:
             seal_data(mask_arena, ks_mask, mask_vals, err, mask_cnt)
-        self._mark(marks, "participate")
+        st = {"P": P, "kidx": kidx_clerk, "ev_openkeys": ev_openkeys, "mask_arena": mask_arena,
+              "ko_mask": ko_mask}
+        if local_clerks:
+            st["inbox"], st["ko_clerk"] = clerk_arena, ko_clerk
+        else:
+            st["clerk_arena"] = clerk_arena
+        return st
 
-        # ---- clerks: verify + decrypt + decode their P boxes, combine
-        main.wait_event(ev_openkeys)
-        inbox = clerk_arena
-        if router is not None:
-            # snapshot transpose over xGMI: boxes travel to the clerks' ranks
-            inbox = router.exchange(clerk_arena)
-            del clerk_arena
-            self._mark(marks, "exchange")
-            ko_clerk = self._open_keys(inbox, kidx_clerk, live, P, err)
+    def _clerk(self, st, live, err):
+        """Open + combine an inbox (the local arena or the routed one)."""
+        spec, n, m = self.spec, self.n, self.m
+        P, B, D, dev = st["P"], spec.batches, spec.dimension, self.device
+        main = torch.cuda.current_stream(dev)
+        main.wait_event(st["ev_openkeys"])
+        inbox = st.pop("inbox")
+        ko_clerk = st.get("ko_clerk") or self._open_keys(inbox, st["kidx"], live, P, err)
         if len(live) == n:
             vals = open_data(inbox, ko_clerk[0], err, out_dtype=self.vdtype)
         else:
@@ -305,14 +368,14 @@ class DeviceAggregator:
         # recipient's share of the mask work is data-parallel too: open these
         # participants' mask boxes and sum them
         mask_sum = None
+        mask_arena = st["mask_arena"]
         if mask_arena is not None:
             mask_sum = torch.empty(D, dtype=torch.int32, device=dev)
-            mvals = open_data(mask_arena, ko_mask, err, out_dtype=torch.int32)
+            mvals = open_data(mask_arena, st["ko_mask"], err, out_dtype=torch.int32)
             if isinstance(spec.masking, FullMask):
                 G.colsum(mvals.view(1, P, D), m, mask_sum)
             else:
                 G.chacha_mask_sum(mvals, D, m, mask_sum, err)
-        self._mark(marks, "clerk")
         return combined, mask_sum
 
     def reduce_partials(self, combined, mask_sum, reducer, marks=None):

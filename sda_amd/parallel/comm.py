@@ -73,6 +73,22 @@ class Comm:
             dist.all_to_all_single(out, w_in, group=self.group)
         return out
 
+    def exchange_async(self, sends, recvs):
+        """Start a point-to-point exchange; returns a handle with ``wait()``.
+
+        With RCCL the grouped send/recv runs on the communicator's stream,
+        which first waits for work already queued on the current stream; the
+        caller keeps queuing compute and calls ``wait()`` (the current stream
+        then waits for the transfer) right before consuming the receives. With
+        gloo the exchange completes before returning.
+        """
+        if not self.device_native or (not sends and not recvs):
+            self.exchange(sends, recvs)
+            return _Done()
+        ops = [dist.P2POp(dist.isend, t.contiguous(), p, group=self.group) for p, t in sends]
+        ops += [dist.P2POp(dist.irecv, t, p, group=self.group) for p, t in recvs]
+        return _Pending(dist.batch_isend_irecv(ops), [t for _, t in sends])
+
     def exchange(self, sends, recvs):
         """Point-to-point exchange: `sends` / `recvs` are lists of (peer, tensor).
 
@@ -104,3 +120,20 @@ class Comm:
         out = [None] * self.world
         dist.all_gather_object(out, obj, group=self.group)
         return out
+
+
+class _Done:
+    def wait(self):
+        pass
+
+
+class _Pending:
+    def __init__(self, works, keep):
+        self.works = works
+        self.keep = keep  # send buffers must outlive the transfer
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
+        self.keep = []

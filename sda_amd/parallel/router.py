@@ -22,6 +22,13 @@ class CommitteeRouter:
     # ---- device arenas --------------------------------------------------------
     def exchange(self, arena):
         """Clerk-major arena [n*P] of this rank's participants -> inbox [n*P]."""
+        inbox, handle = self.exchange_async(arena)
+        handle.wait()
+        return inbox
+
+    def exchange_async(self, arena):
+        """Start the exchange; returns (inbox, handle): ``handle.wait()`` before
+        reading the inbox (the send arena must stay alive until then)."""
         from ..ops.sealed import Arena
 
         P, st, me = self.P, arena.stride, self.comm.rank
@@ -48,9 +55,9 @@ class CommitteeRouter:
                 continue
             bs, ls = rng(t)
             recvs += [(t.peer, inbox.ct[bs]), (t.peer, inbox.pt_len[ls])]
-        self.comm.exchange(sends, recvs)
+        handle = self.comm.exchange_async(sends, recvs)
         self.bytes_sent = sent
-        return inbox
+        return inbox, handle
 
     # ---- host lists -------------------------------------------------------------
     def exchange_host(self, boxes):
