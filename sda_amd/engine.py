@@ -255,36 +255,136 @@ class DeviceAggregator:
                                         waves: int, owner_base: int = 0, marks=None):
         """Committee layout with the exchange hidden behind compute.
 
-        The participants are cut into `waves`; wave w's grouped send/recv runs
-        on the communicator stream while wave w+1 is masked, shared and sealed,
-        and wave w is opened once its transfer has landed. Same result as
-        :meth:`participate_and_clerk` with a router (sums over all waves).
+        X25519 setup is latency-bound (one ladder per thread, ~1.7 ms however
+        few messages), so key agreement is done once per round, not per wave:
+        one seal setup for every box of the round (a wave-blocked clerk-major
+        arena: wave w's n * P_w slots are contiguous), then the 32-byte
+        ephemeral-key headers travel ahead of the data over the same routing
+        plan so the clerks derive all their open keys on the side stream while
+        the waves are being sealed. Per wave: mask + share + seal, grouped
+        send/recv on the communicator stream (overlapping the next wave's
+        compute), open + combine once it has landed.
         """
+        spec, n, m = self.spec, self.n, self.m
         marks = [] if marks is None else marks
-        P = secrets.shape[0]
+        if secrets.dim() != 2 or secrets.shape[1] != spec.dimension:
+            raise ValueError("secrets must be [P][dimension]")
+        secrets = secrets.contiguous()
+        P, D = secrets.shape
+        B, dev = spec.batches, self.device
         bounds = [(P * w // waves, P * (w + 1) // waves) for w in range(waves)]
         bounds = [(lo, hi) for lo, hi in bounds if hi > lo]
-        acc, macc, pending = None, None, None
+        rng_key = native().crypto.random_bytes(32)
+        self._round += 1
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream()
+        pks, sks = self.keys.pks, self.keys.sks
+        KB = G.MSGKEY_BYTES
+
+        arena = Arena.empty(n * P, B, m, dev)
+        inbox = Arena(arena.M, arena.L, arena.modulus, arena.stride, arena.K,
+                      torch.empty_like(arena.ct), torch.empty_like(arena.pt_len))
+        kidx = torch.cat([self._kidx_clerk(hi - lo) for lo, hi in bounds])
+        mask_arena = None
+        if isinstance(spec.masking, FullMask):
+            mask_arena = Arena.empty(P, D, m, dev)
+        elif isinstance(spec.masking, ChaChaMask):
+            mask_arena = Arena.empty(P, spec.masking.seed_words, 0, dev)
+        kidx_rcpt = torch.full((P,), n, dtype=torch.int32, device=dev)
+
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            ks = seal_setup(arena, kidx, pks, rng_key, 0, err)
+            ks_mask = ko_mask = None
+            if mask_arena is not None:
+                ks_mask = seal_setup(mask_arena, kidx_rcpt, pks, rng_key, n * P, err)
+                ko_mask = open_setup(mask_arena, kidx_rcpt, sks, pks, err)
+            ev_seal = torch.cuda.Event()
+            ev_seal.record(side)
+        # caching-allocator stream bookkeeping: side-allocated keys are consumed on
+        # main, main-allocated buffers are touched on side
+        for t in (ks, ks_mask, ko_mask):
+            if t is not None:
+                t.record_stream(main)
+        for t in (arena.ct, kidx, kidx_rcpt) + ((mask_arena.ct,) if mask_arena is not None else ()):
+            t.record_stream(side)
+
+        # ephemeral-key headers ahead of the data (tiny), then the clerks' keys
+        hdr = torch.empty(arena.M, 32, dtype=torch.uint8, device=dev)
+        hdr_in = torch.empty_like(hdr)
+        main.wait_event(ev_seal)
+        hdr.copy_(arena.ct.view(arena.M, arena.stride)[:, :32])
+        sends, recvs = [], []
+        for lo, hi in bounds:
+            s_, r_, _ = router_for(hi - lo).row_ops(hdr, hdr_in, base=n * lo)
+            sends += s_
+            recvs += r_
+        h_hdr = self.comm_exchange(router_for, sends, recvs)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            h_hdr.wait()
+            inbox.ct.view(inbox.M, inbox.stride)[:, :32].copy_(hdr_in)
+            ko = open_setup(inbox, kidx, sks, pks, err)
+            ev_open = torch.cuda.Event()
+            ev_open.record(side)
+        ko.record_stream(main)
+        for t in (hdr_in, inbox.ct, inbox.pt_len):
+            t.record_stream(side)
+        self._mark(marks, "keys")
+
+        acc = macc = None
+        pending = None
 
         def finish(st):
             nonlocal acc, macc
-            st["handle"].wait()
-            comb, msum = self._clerk(st, live, err)
+            lo, hi, handle = st
+            Pw = hi - lo
+            handle.wait()
+            main.wait_event(ev_open)
+            box = inbox.slice(n * lo, n * Pw)
+            kw = ko[n * lo * KB:n * hi * KB]
+            if len(live) == n:
+                vals = open_data(box, kw, err, out_dtype=self.vdtype)
+            else:
+                vals = torch.empty(len(live), Pw, B, dtype=self.vdtype, device=dev)
+                for i, c in enumerate(live):
+                    open_data(box.slice(c * Pw, Pw), kw[c * Pw * KB:(c + 1) * Pw * KB], err,
+                              out=vals[i])
+            comb = torch.empty(len(live), B, dtype=torch.int32, device=dev)
+            G.colsum(vals.view(len(live), Pw, B), m, comb)
             acc = comb if acc is None else acc + comb
-            if msum is not None:
+            if mask_arena is not None:
+                msum = torch.empty(D, dtype=torch.int32, device=dev)
+                mvals = open_data(mask_arena.slice(lo, Pw), ko_mask[lo * KB:hi * KB], err,
+                                  out_dtype=torch.int32)
+                if isinstance(spec.masking, FullMask):
+                    G.colsum(mvals.view(1, Pw, D), m, msum)
+                else:
+                    G.chacha_mask_sum(mvals, D, m, msum, err)
                 macc = msum if macc is None else macc + msum
 
         for lo, hi in bounds:
-            st = self._participate(secrets[lo:hi], live, err, owner_base + lo, local_clerks=False)
-            st["inbox"], st["handle"] = router_for(hi - lo).exchange_async(st["clerk_arena"])
+            Pw = hi - lo
+            shares, cnt, mvals, mcnt = self._share(secrets[lo:hi], rng_key, owner_base + lo, err)
+            box = arena.slice(n * lo, n * Pw)
+            seal_data(box, ks[n * lo * KB:n * hi * KB], shares.view(n * Pw, B), err, cnt)
+            del shares
+            if mask_arena is not None:
+                seal_data(mask_arena.slice(lo, Pw), ks_mask[lo * KB:hi * KB], mvals, err, mcnt)
+            _, handle = router_for(Pw).exchange_async(box, inbox=inbox.slice(n * lo, n * Pw))
             if pending is not None:
                 finish(pending)
-            pending = st
+            pending = (lo, hi, handle)
         finish(pending)
         self._mark(marks, "clerk")
-        m = self.m
-        return (torch.remainder(acc, m) if len(bounds) > 1 else acc,
-                torch.remainder(macc, m) if (macc is not None and len(bounds) > 1) else macc)
+        multi = len(bounds) > 1
+        return (torch.remainder(acc, m) if multi else acc,
+                torch.remainder(macc, m) if (macc is not None and multi) else macc)
+
+    @staticmethod
+    def comm_exchange(router_for, sends, recvs):
+        """Grouped P2P through the routers' communicator (any wave size's router)."""
+        return router_for(None).comm.exchange_async(sends, recvs) if sends or recvs else _NoWait()
 
     def _participate(self, secrets, live, err, owner_base, local_clerks: bool):
         """Mask + share + seal one batch of participants; returns the state the
@@ -495,6 +595,11 @@ class DeviceAggregator:
             cache[key] = torch.tensor(self._pss.lagrange_matrix(list(live)), dtype=torch.int64).to(
                 torch.int32).to(self.device)
         return cache[key]
+
+
+class _NoWait:
+    def wait(self):
+        pass
 
 
 def describe_error(e: int) -> str:

@@ -112,9 +112,15 @@ class DistributedAggregator:
         out = self.comm.reduce_sum(wire)
         return None if out is None else out.to(torch.int64)
 
-    def router(self, P: int):
+    def router(self, P):
+        """Committee router for waves of P participants (P=None: any router,
+        for plan-independent transfers through the communicator)."""
         if self.layout != "committee":
             return None
+        if P is None:
+            from types import SimpleNamespace
+
+            return SimpleNamespace(comm=self.comm)
         if P not in self._routers:
             from .router import CommitteeRouter
 
