@@ -309,28 +309,31 @@ class DeviceAggregator:
         for t in (arena.ct, kidx, kidx_rcpt) + ((mask_arena.ct,) if mask_arena is not None else ()):
             t.record_stream(side)
 
-        # ephemeral-key headers ahead of the data (tiny), then the clerks' keys
-        hdr = torch.empty(arena.M, 32, dtype=torch.uint8, device=dev)
-        hdr_in = torch.empty_like(hdr)
-        main.wait_event(ev_seal)
-        hdr.copy_(arena.ct.view(arena.M, arena.stride)[:, :32])
-        sends, recvs = [], []
-        for lo, hi in bounds:
-            s_, r_, _ = router_for(hi - lo).row_ops(hdr, hdr_in, base=n * lo)
-            sends += s_
-            recvs += r_
-        h_hdr = self.comm_exchange(router_for, sends, recvs)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            h_hdr.wait()
-            inbox.ct.view(inbox.M, inbox.stride)[:, :32].copy_(hdr_in)
-            ko = open_setup(inbox, kidx, sks, pks, err)
-            ev_open = torch.cuda.Event()
-            ev_open.record(side)
-        ko.record_stream(main)
-        for t in (hdr_in, inbox.ct, inbox.pt_len):
-            t.record_stream(side)
-        self._mark(marks, "keys")
+        def start_headers():
+            """Ephemeral-key headers ahead of the data (tiny), then the clerks'
+            open keys on the side stream; returns the event to wait on."""
+            hdr = torch.empty(arena.M, 32, dtype=torch.uint8, device=dev)
+            hdr_in = torch.empty_like(hdr)
+            main.wait_event(ev_seal)
+            hdr.copy_(arena.ct.view(arena.M, arena.stride)[:, :32])
+            sends, recvs = [], []
+            for lo, hi in bounds:
+                s_, r_, _ = router_for(hi - lo).row_ops(hdr, hdr_in, base=n * lo)
+                sends += s_
+                recvs += r_
+            h_hdr = self.comm_exchange(router_for, sends, recvs)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                h_hdr.wait()
+                inbox.ct.view(inbox.M, inbox.stride)[:, :32].copy_(hdr_in)
+                keys = open_setup(inbox, kidx, sks, pks, err)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            keys.record_stream(main)
+            for t in (hdr, hdr_in, inbox.ct, inbox.pt_len):
+                t.record_stream(side)
+            self._mark(marks, "keys")
+            return keys, ev
 
         acc = macc = None
         pending = None
@@ -363,9 +366,12 @@ class DeviceAggregator:
                     G.chacha_mask_sum(mvals, D, m, msum, err)
                 macc = msum if macc is None else macc + msum
 
+        ko = ev_open = None
         for lo, hi in bounds:
             Pw = hi - lo
             shares, cnt, mvals, mcnt = self._share(secrets[lo:hi], rng_key, owner_base + lo, err)
+            if ko is None:  # the first wave's shares overlap the whole-round seal setup
+                ko, ev_open = start_headers()
             box = arena.slice(n * lo, n * Pw)
             seal_data(box, ks[n * lo * KB:n * hi * KB], shares.view(n * Pw, B), err, cnt)
             del shares

@@ -53,7 +53,8 @@ class DistributedAggregator:
     """
 
     def __init__(self, spec: AggregationSpec, engine: str = "device", device=None, group=None,
-                 time_stages: bool = False, layout: str = "committee", waves: int = 4):
+                 time_stages: bool = False, layout: str = "committee", waves: int = 4,
+                 force_pipeline: bool = False):
         self.spec = spec
         self.comm = Comm(group)
         self.rank, self.world = self.comm.rank, self.comm.world
@@ -85,6 +86,7 @@ class DistributedAggregator:
             raise ValueError("layout must be 'committee' or 'owner'")
         self.layout = layout
         self.waves = max(1, waves)  # committee layout: exchange pipelined over participant waves
+        self.force_pipeline = force_pipeline  # pipeline even on one rank (overhead measurement)
         self._routers = {}
 
     def _shared_keys(self, count: int) -> np.ndarray:
@@ -135,7 +137,8 @@ class DistributedAggregator:
         plan cuts each clerk's P boxes into fixed parts).
         """
         P = int(secrets_local.shape[0])
-        if self.kind == "device" and self.layout == "committee" and self.world > 1:
+        if self.kind == "device" and self.layout == "committee" and (self.world > 1 or
+                                                                      self.force_pipeline):
             return self.engine.run_round(secrets_local, clerks=clerks, check=check,
                                          reducer=self._reduce, owner_base=_owner_base(self.rank),
                                          router_for=self.router, waves=min(self.waves, P))
