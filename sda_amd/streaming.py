@@ -36,10 +36,12 @@ class StreamResult:
 
 class StreamingAggregator:
     def __init__(self, engine: DeviceAggregator, wave: int = 64,
-                 checkpoint: Optional[str] = None, checkpoint_every: int = 8):
+                 checkpoint: Optional[str] = None, checkpoint_every: int = 8,
+                 inner_waves: int = 4):
         if wave <= 0:
             raise ValueError("wave must be positive")
         self.engine = engine
+        self.inner_waves = max(1, inner_waves)
         self.wave = wave
         self.checkpoint = checkpoint
         self.every = max(1, checkpoint_every)
@@ -112,9 +114,16 @@ class StreamingAggregator:
             first = w * self.wave
             count = min(self.wave, total - first)
             x = make_wave(w, first, count)
-            router = router_for(count) if router_for is not None else None
-            comb, msum = eng.participate_and_clerk(x, live, err, owner_base=owner_base + first,
-                                                   router=router)
+            if router_for is not None and count >= 2:
+                # committee layout: the exchange is pipelined inside the wave
+                comb, msum = eng.participate_and_clerk_pipelined(
+                    x, live, err, router_for, waves=min(self.inner_waves, count),
+                    owner_base=owner_base + first)
+            else:
+                router = router_for(count) if router_for is not None else None
+                comb, msum = eng.participate_and_clerk(x, live, err,
+                                                       owner_base=owner_base + first,
+                                                       router=router)
             acc += comb
             if mask_acc is not None:
                 mask_acc += msum
