@@ -35,13 +35,18 @@ def _worker(rank, world, port, name, layout, q):
                 "additive2": AggregationSpec(D, m, Additive(2, m)),
                 "pss": AggregationSpec(D, m, PSS_4_8_3)}[name]
         agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", 0),
-                                    layout=layout)
+                                    layout="committee" if layout == "stream" else layout)
 
         def inputs(r):
             g = torch.Generator().manual_seed(99 + r)
             return torch.randint(0, m, (P, D), dtype=torch.int32, generator=g)
 
-        res = agg.run_round(inputs(rank).cuda())
+        if layout == "stream":
+            # streamed committee round: waves of 4, pipelined exchange inside each wave
+            res = agg.run_streamed(P, lambda w, first, count: inputs(rank)[first:first + count].cuda(),
+                                   wave=4)
+        else:
+            res = agg.run_round(inputs(rank).cuda())
         if rank == 0:
             ref = torch.remainder(sum(inputs(r).to(torch.int64).sum(0) for r in range(world)), m)
             q.put(("ok", bool(torch.equal(res.output.cpu().to(torch.int64), ref))))
@@ -55,7 +60,8 @@ def _worker(rank, world, port, name, layout, q):
 @pytest.mark.parametrize("world,name,layout", [(2, "fullmask", "committee"),
                                                (2, "pss", "committee"),
                                                (2, "fullmask", "owner"),
-                                               (3, "additive2", "committee")])
+                                               (3, "additive2", "committee"),
+                                               (3, "fullmask", "stream")])
 def test_distributed_device_ranks_one_gpu(cuda, world, name, layout):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
