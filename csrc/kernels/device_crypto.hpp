@@ -116,6 +116,8 @@ enum RngPurpose : uint64_t {
   kPurposeMaskRetry = 4,
   kPurposeChaChaSeed = 5,
   kPurposeEphemeral = 6,
+  kPurposeShares16 = 7,   // 16-bit share draws (two rows per ChaCha block)
+  kPurposeRetry16 = 8,    // lane-private replacements for rejected 16-bit draws
 };
 SDA_DEV uint64_t stream_id(uint64_t purpose, uint64_t owner) { return (purpose << 56) | owner; }
 

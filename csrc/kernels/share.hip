@@ -232,6 +232,159 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+// ------------------------------------------------ additive, 16-bit draws ----
+// For m < 2^16 one ChaCha block yields 32 draws (its 16-bit halves) instead of
+// 16, halving the keystream work of the largest participant kernel. Each lane
+// covers 64 elements (4 count tiles of 4096 per block: lane l, group g ->
+// elements blk*16384 + g*4096 + l*16 .. +15) and every row pair of draws costs
+// one block per group. A rejected half (probability (2^16 mod m) / 2^16, 0.23%
+// for m = 433) is used provisionally and recorded; after all rows the lane
+// replaces it from a private retry stream and patches the stored share, the
+// final share and the tile byte counts -- so each lane pays at most one extra
+// block, and every share stays an exact, independent uniform draw.
+constexpr int kG16 = 4;             // groups of 16 elements per lane
+constexpr int kFix16 = 4;           // rejections remembered per lane (more: inline fixup)
+constexpr int kMaxRows16 = 64;      // rows (n - 1 draws + mask) handled by this kernel
+
+SDA_DEV uint32_t half16(const uint32_t (&w)[16], int k) { return (w[k >> 1] >> (16 * (k & 1))) & 0xffffu; }
+
+struct Retry16 {
+  RngKey rk;
+  uint64_t owner, lane_id;
+  uint32_t w[16];
+  int used = 32;
+  uint32_t blk = 0;
+  SDA_DEV uint32_t next(uint32_t zone16, const ModParams& mp) {
+    for (;;) {
+      if (used == 32) {
+        rng_block(w, rk, stream_id(kPurposeRetry16, owner), (lane_id << 8) | blk++);
+        used = 0;
+      }
+      // select chain instead of w[used >> 1]: no dynamic register indexing (scratch)
+      uint32_t word = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) word = (k == (used >> 1)) ? w[k] : word;
+      const uint32_t x = (word >> (16 * (used & 1))) & 0xffffu;
+      ++used;
+      if (x < zone16) return mod32(x, mp);
+    }
+  }
+};
+
+template <int MASK>
+__global__ void __launch_bounds__(kBlock)
+    k_share_additive16(int P, int D, int n, ModParams mp, uint32_t zone16,
+                       const int32_t* __restrict__ secrets, RngKeyArg rng, uint64_t owner_base,
+                       uint16_t* __restrict__ shares, uint32_t* __restrict__ cnt,
+                       uint32_t* __restrict__ mask_out, uint32_t* __restrict__ mask_cnt) {
+  // rows: [mask] + n-1 random shares; partial[row][group][wave] byte counts, last row
+  // (the final share) at index kMaxRows16
+  __shared__ int partial[kMaxRows16 + 1][kG16][kWaves];
+  const int blk = blockIdx.x, p = blockIdx.y;
+  const int T = (D + kTileValues - 1) / kTileValues;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint64_t owner = owner_base + (uint64_t)p;
+  const RngKey rk = to_key(rng);
+  const uint32_t m = mp.m;
+  const bool vec_ok = (D % 16) == 0;
+  constexpr int kMaskRows = MASK == kMaskFull ? 1 : 0;
+  const int rows = kMaskRows + (n - 1);
+  const int64_t Gtot = ((int64_t)D + 15) / 16;
+
+  uint32_t fix[kFix16] = {0, 0, 0, 0};  // (row << 24) | (g << 20) | (i << 16) | bad
+  int nfix = 0;
+  Retry16 retry{rk, owner, (uint64_t)(blk * kBlock + tid)};
+  uint16_t* lastrow = shares + ((size_t)(n - 1) * P + p) * D;
+
+  // group-outer: only the current group's 16 running "last" values are live
+#pragma unroll 1
+  for (int g = 0; g < kG16; ++g) {
+    const int e0 = blk * (kG16 * kTileValues) + g * kTileValues + tid * 16;
+    const int valid = max(0, min(16, D - e0));
+    uint32_t last[16];
+    load16_secrets(last, secrets + (size_t)p * D + e0, valid, vec_ok, mp);
+    for (int q = 0; 2 * q < rows; ++q) {
+      uint32_t w[16];
+      rng_block(w, rk, stream_id(kPurposeShares16, owner), (uint64_t)q * Gtot + e0 / 16);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = 2 * q + h;
+        if (row >= rows) break;
+        const bool is_mask = row < kMaskRows;
+        uint32_t v[16];
+        uint32_t bytes = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t x = half16(w, 16 * h + i);
+          v[i] = mod32(x, mp);
+          if (x >= zone16 && i < valid) {  // rare: keep provisionally, fix below
+            const uint32_t rec = ((uint32_t)row << 24) | ((uint32_t)g << 20) | ((uint32_t)i << 16) | v[i];
+            if (nfix < kFix16) {
+#pragma unroll
+              for (int k = 0; k < kFix16; ++k) fix[k] = (k == nfix) ? rec : fix[k];
+              ++nfix;
+            } else {
+              v[i] = retry.next(zone16, mp);  // overflow: replace right away
+            }
+          }
+          last[i] = is_mask ? add_mod(last[i], v[i], m) : sub_mod(last[i], v[i], m);
+          bytes += i < valid ? vlen(v[i]) : 0u;
+        }
+        if (is_mask) {
+          store16<uint32_t>(mask_out + (size_t)p * D + e0, v, valid, vec_ok);
+        } else {
+          store16<uint16_t>(shares + ((size_t)(row - kMaskRows) * P + p) * D + e0, v, valid,
+                            vec_ok);
+        }
+        bytes = wave_sum(bytes);
+        if (lane == 0) partial[row][g][wave] = (int)bytes;
+      }
+    }
+    // replacements for this group's rejected draws, while `last` is still live
+    if (nfix > 0) {
+#pragma unroll
+      for (int k = 0; k < kFix16; ++k) {
+        if (k >= nfix) break;
+        const uint32_t rec = fix[k];
+        const int row = (int)(rec >> 24), i = (int)((rec >> 16) & 15);
+        const uint32_t bad = rec & 0xffffu;
+        const uint32_t repl = retry.next(zone16, mp);
+        const bool is_mask = row < kMaskRows;
+#pragma unroll
+        for (int ii = 0; ii < 16; ++ii)
+          if (ii == i)
+            last[ii] = is_mask ? add_mod(sub_mod(last[ii], bad, m), repl, m)
+                               : sub_mod(add_mod(last[ii], bad, m), repl, m);
+        if (is_mask) mask_out[(size_t)p * D + e0 + i] = repl;
+        else shares[((size_t)(row - kMaskRows) * P + p) * D + e0 + i] = (uint16_t)repl;
+        atomicAdd(&partial[row][g][wave], (int)vlen(repl) - (int)vlen(bad));
+      }
+      nfix = 0;
+    }
+    // the final share of this group
+    uint32_t bytes = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bytes += i < valid ? vlen(last[i]) : 0u;
+    store16<uint16_t>(lastrow + e0, last, valid, vec_ok);
+    bytes = wave_sum(bytes);
+    if (lane == 0) partial[kMaxRows16][g][wave] = (int)bytes;
+  }
+  __syncthreads();
+  // tile byte counts: rows x 4 groups (each group is one count tile)
+  for (int x = tid; x < (rows + 1) * kG16; x += kBlock) {
+    const int r = x / kG16, g = x % kG16;
+    const int prow = r < rows ? r : kMaxRows16;
+    const int t = blk * kG16 + g;
+    if (t >= T) continue;
+    int s = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += partial[prow][g][w];
+    if (r < kMaskRows) mask_cnt[(size_t)p * T + t] = (uint32_t)s;
+    else if (r < rows) cnt[((size_t)(r - kMaskRows) * P + p) * T + t] = (uint32_t)s;
+    else cnt[((size_t)(n - 1) * P + p) * T + t] = (uint32_t)s;
+  }
+}
+
 // --------------------------------------------------------- packed Shamir ----
 constexpr int kPssMaxK = 8;
 constexpr int kPssMaxT = 16;
@@ -410,6 +563,21 @@ void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, con
   if (mask_mode == kMaskChaCha)
     hipLaunchKernelGGL(k_chacha_seeds, dim3((P + 63) / 64), dim3(64), 0, s, P, seed_words, rng,
                        owner_base, seeds);
+  // 16-bit draws: u16 shares, no ChaCha mask, room for the rows in LDS
+  if (value_bytes == 2 && m < 65536u && mask_mode != kMaskChaCha &&
+      (n - 1) + (mask_mode == kMaskFull ? 1 : 0) <= kMaxRows16) {
+    const uint32_t zone16 = 65536u - (65536u % m);
+    dim3 grid16((D + kG16 * kTileValues - 1) / (kG16 * kTileValues), P);
+    if (mask_mode == kMaskFull)
+      hipLaunchKernelGGL(k_share_additive16<kMaskFull>, grid16, dim3(kBlock), 0, s, P, D, n, mp,
+                         zone16, secrets, rng, owner_base, (uint16_t*)shares, cnt, mask_out,
+                         mask_cnt);
+    else
+      hipLaunchKernelGGL(k_share_additive16<kMaskNone>, grid16, dim3(kBlock), 0, s, P, D, n, mp,
+                         zone16, secrets, rng, owner_base, (uint16_t*)shares, cnt, mask_out,
+                         mask_cnt);
+    return;
+  }
   dim3 grid((D + kTileValues - 1) / kTileValues, P);
 #define SDA_ADD_LAUNCH(VT, MK)                                                                \
   hipLaunchKernelGGL((k_share_additive<VT, MK>), grid, dim3(kBlock), 0, s, P, D, n, mp,        \

@@ -1,0 +1,54 @@
+"""Additive share kernel with 16-bit draws (k_share_additive16): exactness under
+heavy rejection (m = 40000 rejects 39% of the halves, exercising the deferred
+and the overflow replacement paths), byte counts, masks, and uniformity."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(m, n, P, D, mask):
+    from sda_amd.ops import gpu as G
+
+    g = torch.Generator(device="cuda").manual_seed(m + n)
+    secrets = torch.randint(-m, m, (P, D), dtype=torch.int32, device="cuda", generator=g)
+    shares = torch.empty(n, P, D, dtype=torch.int16, device="cuda")
+    cnt = torch.empty(n * P * G.tiles(D), dtype=torch.int32, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    mask_out = torch.empty(P, D, dtype=torch.int32, device="cuda") if mask else None
+    mask_cnt = torch.empty(P * G.tiles(D), dtype=torch.int32, device="cuda") if mask else None
+    G.share_additive(secrets, n, m, shares, cnt, G.MASK_FULL if mask else G.MASK_NONE,
+                     bytes(range(32)), 0, mask_out=mask_out, mask_cnt=mask_cnt, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    sh = shares.to(torch.int64) & 0xFFFF
+    assert int(sh.max()) < m
+    total = torch.remainder(sh.sum(0), m)
+    expect = torch.remainder(secrets.to(torch.int64) + (mask_out.to(torch.int64) if mask else 0), m)
+    assert torch.equal(total, expect)
+    # tile byte counts equal a recount of the stored values
+    recount = torch.empty_like(cnt)
+    G.count(shares.view(n * P, D), recount)
+    assert torch.equal(cnt, recount)
+    if mask:
+        assert int(mask_out.max()) < m and int(mask_out.min()) >= 0
+        mrecount = torch.empty_like(mask_cnt)
+        G.count(mask_out, mrecount)
+        assert torch.equal(mask_cnt, mrecount)
+    return sh
+
+
+@pytest.mark.parametrize("m", [433, 40000, 65521, 2])
+@pytest.mark.parametrize("n,mask", [(3, False), (2, True), (5, True), (8, False)])
+def test_share16_exact(cuda, m, n, mask):
+    _run(m, n, 3, 70001, mask)  # D not a multiple of the 16384-element block
+
+
+def test_share16_uniform_under_rejection(cuda):
+    m = 40000
+    sh = _run(m, 3, 16, 200000, False)
+    row = sh[0].reshape(-1).float()
+    buckets = torch.histc(row, bins=20, min=0, max=m)
+    expected = row.numel() / 20
+    chi2 = float(((buckets - expected) ** 2 / expected).sum())
+    assert chi2 < 60, chi2  # 19 degrees of freedom; p < 1e-5 beyond ~50
