@@ -108,6 +108,7 @@ PYBIND11_MODULE(_sda_gpu, m) {
                            P<uint32_t>(mask_cnt), P<uint32_t>(seeds), P<uint32_t>(err), S(stream));
           check_launch("share_pss");
         });
+  m.def("set_share16", &set_share16, "use the 16-bit-draw additive share kernel (benchmarking)");
   m.def("count", [](int M, int L, int value_bytes, uintptr_t vals, uintptr_t cnt, uintptr_t stream) {
     launch_count(M, L, value_bytes, P<const void>(vals), P<uint32_t>(cnt), S(stream));
     check_launch("count");

@@ -73,6 +73,9 @@ void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, con
                            void* shares, uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt,
                            uint32_t* seeds, uint32_t* err, hipStream_t s);
 
+// Select the 16-bit-draw additive kernel (default on) -- benchmarking switch.
+void set_share16(int mode);
+
 // Packed Shamir: shares = M . [s_1..s_k, r_1..r_t] mod p per batch (M: n x (k+t)
 // host-computed from the tss FFT construction).
 void launch_share_pss(int P, int D, int n, int k, int t, uint32_t p, int value_bytes,

@@ -236,50 +236,27 @@ __global__ void __launch_bounds__(kBlock)
 // For m < 2^16 one ChaCha block yields 32 draws (its 16-bit halves) instead of
 // 16, halving the keystream work of the largest participant kernel. Each lane
 // covers 64 elements (4 count tiles of 4096 per block: lane l, group g ->
-// elements blk*16384 + g*4096 + l*16 .. +15) and every row pair of draws costs
-// one block per group. A rejected half (probability (2^16 mod m) / 2^16, 0.23%
-// for m = 433) is used provisionally and recorded; after all rows the lane
-// replaces it from a private retry stream and patches the stored share, the
-// final share and the tile byte counts -- so each lane pays at most one extra
-// block, and every share stays an exact, independent uniform draw.
-constexpr int kG16 = 4;             // groups of 16 elements per lane
-constexpr int kFix16 = 4;           // rejections remembered per lane (more: inline fixup)
-constexpr int kMaxRows16 = 64;      // rows (n - 1 draws + mask) handled by this kernel
+// elements blk*16384 + g*4096 + l*16 .. +15); every row pair of draws costs one
+// block per group. A rejected half (probability (2^16 mod m) / 2^16: 0.23% for
+// m = 433) is replaced on the spot by the next accepted half of the lane's
+// private retry block, generated once per lane and kept in registers; a lane
+// that exhausts its 32 spares falls back to the per-element retry stream. Every
+// share stays an exact, independent uniform draw. (A deferred variant that
+// patched stores after the fact needed an out-of-line call whose ABI cost more
+// registers than the halved keystream saved.)
+constexpr int kG16 = 4;        // groups of 16 elements per lane
+constexpr int kMaxRows16 = 64; // rows (n - 1 draws + mask) handled by this kernel
 
 SDA_DEV uint32_t half16(const uint32_t (&w)[16], int k) { return (w[k >> 1] >> (16 * (k & 1))) & 0xffffu; }
 
-struct Retry16 {
-  RngKey rk;
-  uint64_t owner, lane_id;
-  uint32_t w[16];
-  int used = 32;
-  uint32_t blk = 0;
-  SDA_DEV uint32_t next(uint32_t zone16, const ModParams& mp) {
-    for (;;) {
-      if (used == 32) {
-        rng_block(w, rk, stream_id(kPurposeRetry16, owner), (lane_id << 8) | blk++);
-        used = 0;
-      }
-      // select chain instead of w[used >> 1]: no dynamic register indexing (scratch)
-      uint32_t word = 0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) word = (k == (used >> 1)) ? w[k] : word;
-      const uint32_t x = (word >> (16 * (used & 1))) & 0xffffu;
-      ++used;
-      if (x < zone16) return mod32(x, mp);
-    }
-  }
-};
-
 template <int MASK>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
     k_share_additive16(int P, int D, int n, ModParams mp, uint32_t zone16,
                        const int32_t* __restrict__ secrets, RngKeyArg rng, uint64_t owner_base,
                        uint16_t* __restrict__ shares, uint32_t* __restrict__ cnt,
                        uint32_t* __restrict__ mask_out, uint32_t* __restrict__ mask_cnt) {
-  // rows: [mask] + n-1 random shares; partial[row][group][wave] byte counts, last row
-  // (the final share) at index kMaxRows16
-  __shared__ int partial[kMaxRows16 + 1][kG16][kWaves];
+  // partial[row][group][wave] byte counts; the final share at index kMaxRows16
+  __shared__ uint32_t partial[kMaxRows16 + 1][kG16][kWaves];
   const int blk = blockIdx.x, p = blockIdx.y;
   const int T = (D + kTileValues - 1) / kTileValues;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -290,13 +267,13 @@ __global__ void __launch_bounds__(kBlock)
   constexpr int kMaskRows = MASK == kMaskFull ? 1 : 0;
   const int rows = kMaskRows + (n - 1);
   const int64_t Gtot = ((int64_t)D + 15) / 16;
+  const uint64_t lane_id = (uint64_t)blk * kBlock + tid;
 
-  uint32_t fix[kFix16] = {0, 0, 0, 0};  // (row << 24) | (g << 20) | (i << 16) | bad
-  int nfix = 0;
-  Retry16 retry{rk, owner, (uint64_t)(blk * kBlock + tid)};
+  uint32_t rw[16];  // this lane's spare halves
+  rng_block(rw, rk, stream_id(kPurposeRetry16, owner), lane_id);
+  uint32_t rused = 0;
   uint16_t* lastrow = shares + ((size_t)(n - 1) * P + p) * D;
 
-  // group-outer: only the current group's 16 running "last" values are live
 #pragma unroll 1
   for (int g = 0; g < kG16; ++g) {
     const int e0 = blk * (kG16 * kTileValues) + g * kTileValues + tid * 16;
@@ -312,21 +289,35 @@ __global__ void __launch_bounds__(kBlock)
         if (row >= rows) break;
         const bool is_mask = row < kMaskRows;
         uint32_t v[16];
-        uint32_t bytes = 0;
+        uint32_t rej = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const uint32_t x = half16(w, 16 * h + i);
           v[i] = mod32(x, mp);
-          if (x >= zone16 && i < valid) {  // rare: keep provisionally, fix below
-            const uint32_t rec = ((uint32_t)row << 24) | ((uint32_t)g << 20) | ((uint32_t)i << 16) | v[i];
-            if (nfix < kFix16) {
+          rej |= (uint32_t)(x >= zone16) << i;
+        }
+        if (rej) {  // rare per lane (~4% of rows at m = 433)
+          for (uint32_t bits = rej; bits; bits &= bits - 1) {
+            const int i = __builtin_ctz(bits);
+            uint32_t x = 0xffffffffu;
+            while (rused < 32 && x >= zone16) {
+              uint32_t word = 0;
 #pragma unroll
-              for (int k = 0; k < kFix16; ++k) fix[k] = (k == nfix) ? rec : fix[k];
-              ++nfix;
-            } else {
-              v[i] = retry.next(zone16, mp);  // overflow: replace right away
+              for (int k = 0; k < 16; ++k) word = (k == (int)(rused >> 1)) ? rw[k] : word;
+              x = (word >> (16 * (rused & 1))) & 0xffffu;
+              ++rused;
             }
+            const uint32_t r = x < zone16
+                ? mod32(x, mp)
+                : uniform_fixup(rk, kPurposeSharesRetry, owner, ((uint64_t)row << 40) | (uint64_t)(e0 + i), m,
+                                (uint32_t)mp.zone32);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = k == i ? r : v[k];
           }
+        }
+        uint32_t bytes = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
           last[i] = is_mask ? add_mod(last[i], v[i], m) : sub_mod(last[i], v[i], m);
           bytes += i < valid ? vlen(v[i]) : 0u;
         }
@@ -337,29 +328,8 @@ __global__ void __launch_bounds__(kBlock)
                             vec_ok);
         }
         bytes = wave_sum(bytes);
-        if (lane == 0) partial[row][g][wave] = (int)bytes;
+        if (lane == 0) partial[row][g][wave] = bytes;
       }
-    }
-    // replacements for this group's rejected draws, while `last` is still live
-    if (nfix > 0) {
-#pragma unroll
-      for (int k = 0; k < kFix16; ++k) {
-        if (k >= nfix) break;
-        const uint32_t rec = fix[k];
-        const int row = (int)(rec >> 24), i = (int)((rec >> 16) & 15);
-        const uint32_t bad = rec & 0xffffu;
-        const uint32_t repl = retry.next(zone16, mp);
-        const bool is_mask = row < kMaskRows;
-#pragma unroll
-        for (int ii = 0; ii < 16; ++ii)
-          if (ii == i)
-            last[ii] = is_mask ? add_mod(sub_mod(last[ii], bad, m), repl, m)
-                               : sub_mod(add_mod(last[ii], bad, m), repl, m);
-        if (is_mask) mask_out[(size_t)p * D + e0 + i] = repl;
-        else shares[((size_t)(row - kMaskRows) * P + p) * D + e0 + i] = (uint16_t)repl;
-        atomicAdd(&partial[row][g][wave], (int)vlen(repl) - (int)vlen(bad));
-      }
-      nfix = 0;
     }
     // the final share of this group
     uint32_t bytes = 0;
@@ -367,21 +337,21 @@ __global__ void __launch_bounds__(kBlock)
     for (int i = 0; i < 16; ++i) bytes += i < valid ? vlen(last[i]) : 0u;
     store16<uint16_t>(lastrow + e0, last, valid, vec_ok);
     bytes = wave_sum(bytes);
-    if (lane == 0) partial[kMaxRows16][g][wave] = (int)bytes;
+    if (lane == 0) partial[kMaxRows16][g][wave] = bytes;
   }
   __syncthreads();
-  // tile byte counts: rows x 4 groups (each group is one count tile)
+  // tile byte counts: (rows + final) x 4 groups, each group one count tile
   for (int x = tid; x < (rows + 1) * kG16; x += kBlock) {
     const int r = x / kG16, g = x % kG16;
     const int prow = r < rows ? r : kMaxRows16;
     const int t = blk * kG16 + g;
     if (t >= T) continue;
-    int s = 0;
+    uint32_t s = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) s += partial[prow][g][w];
-    if (r < kMaskRows) mask_cnt[(size_t)p * T + t] = (uint32_t)s;
-    else if (r < rows) cnt[((size_t)(r - kMaskRows) * P + p) * T + t] = (uint32_t)s;
-    else cnt[((size_t)(n - 1) * P + p) * T + t] = (uint32_t)s;
+    if (r < kMaskRows) mask_cnt[(size_t)p * T + t] = s;
+    else if (r < rows) cnt[((size_t)(r - kMaskRows) * P + p) * T + t] = s;
+    else cnt[((size_t)(n - 1) * P + p) * T + t] = s;
   }
 }
 
@@ -553,6 +523,9 @@ __global__ void __launch_bounds__(kBlock)
 
 }  // namespace
 
+static int g_share16 = 1;
+void set_share16(int mode) { g_share16 = mode; }
+
 void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, const int32_t* secrets,
                            int mask_mode, int seed_words, RngKeyArg rng, uint64_t owner_base,
                            void* shares, uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt,
@@ -564,7 +537,7 @@ void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, con
     hipLaunchKernelGGL(k_chacha_seeds, dim3((P + 63) / 64), dim3(64), 0, s, P, seed_words, rng,
                        owner_base, seeds);
   // 16-bit draws: u16 shares, no ChaCha mask, room for the rows in LDS
-  if (value_bytes == 2 && m < 65536u && mask_mode != kMaskChaCha &&
+  if (g_share16 && value_bytes == 2 && m < 65536u && mask_mode != kMaskChaCha &&
       (n - 1) + (mask_mode == kMaskFull ? 1 : 0) <= kMaxRows16) {
     const uint32_t zone16 = 65536u - (65536u % m);
     dim3 grid16((D + kG16 * kTileValues - 1) / (kG16 * kTileValues), P);
