@@ -66,18 +66,24 @@ PYBIND11_MODULE(_sda_gpu, m) {
 
   m.def("seal_setup", [](int M, std::vector<uint32_t> rng, uint64_t owner_base, uintptr_t key_idx,
                          uintptr_t pks, uintptr_t ct, uint64_t stride, uintptr_t keys,
-                         uintptr_t err, uintptr_t stream) {
+                         uintptr_t err, uintptr_t gate, uint32_t gate_val, uintptr_t stream) {
     launch_seal_setup(M, rng_from(rng), owner_base, P<const uint32_t>(key_idx),
                       P<const uint32_t>(pks), P<uint8_t>(ct), stride, P<MsgKey>(keys),
-                      P<uint32_t>(err), S(stream));
+                      P<uint32_t>(err), P<uint32_t>(gate), gate_val, S(stream));
     check_launch("seal_setup");
   });
   m.def("open_setup", [](int M, uintptr_t key_idx, uintptr_t sks, uintptr_t pks, uintptr_t ct,
-                         uint64_t stride, uintptr_t keys, uintptr_t err, uintptr_t stream) {
+                         uint64_t stride, uintptr_t keys, uintptr_t err, uintptr_t gate,
+                         uint32_t gate_val, uintptr_t stream) {
     launch_open_setup(M, P<const uint32_t>(key_idx), P<const uint32_t>(sks),
                       P<const uint32_t>(pks), P<const uint8_t>(ct), stride, P<MsgKey>(keys),
-                      P<uint32_t>(err), S(stream));
+                      P<uint32_t>(err), P<uint32_t>(gate), gate_val, S(stream));
     check_launch("open_setup");
+  });
+  m.def("gate_wait", [](uintptr_t gate, uint32_t val, uint32_t timeout_us, uintptr_t stream) {
+    if (gate == 0) throw std::invalid_argument("gate_wait: null gate");
+    launch_gate_wait(P<const uint32_t>(gate), val, timeout_us, S(stream));
+    check_launch("gate_wait");
   });
   m.def("x25519", [](int N, uintptr_t sc, uintptr_t pt, uintptr_t out, uintptr_t stream) {
     launch_x25519(N, P<const uint32_t>(sc), P<const uint32_t>(pt), P<uint32_t>(out), S(stream));
@@ -129,10 +135,14 @@ PYBIND11_MODULE(_sda_gpu, m) {
                           P<const MsgKey>(keys), P<uint8_t>(ct), stride, S(stream));
     check_launch("encode_encrypt");
   });
-  m.def("mac_chunks", [](int M, int K, uintptr_t keys, uintptr_t ct, uint64_t stride,
-                         uintptr_t pt_len, uintptr_t partials, int decrypt, uintptr_t term_cnt,
-                         uintptr_t stream) {
-    launch_mac_chunks(M, K, P<const MsgKey>(keys), P<uint8_t>(ct), stride,
+  m.def("poly_powers", [](int M, uintptr_t keys, uintptr_t pows, uintptr_t stream) {
+    launch_poly_powers(M, P<const MsgKey>(keys), P<uint32_t>(pows), S(stream));
+    check_launch("poly_powers");
+  });
+  m.def("mac_chunks", [](int M, int K, uintptr_t keys, uintptr_t pows, uintptr_t ct,
+                         uint64_t stride, uintptr_t pt_len, uintptr_t partials, int decrypt,
+                         uintptr_t term_cnt, uintptr_t stream) {
+    launch_mac_chunks(M, K, P<const MsgKey>(keys), P<const uint32_t>(pows), P<uint8_t>(ct), stride,
                       P<const uint32_t>(pt_len), P<uint32_t>(partials), decrypt,
                       P<uint32_t>(term_cnt), S(stream));
     check_launch("mac_chunks");

@@ -50,11 +50,16 @@ struct RngKeyArg {
 // msg_owner_base + j), epk -> header, MsgKey for encryption.
 void launch_seal_setup(int M, RngKeyArg rng, uint64_t msg_owner_base, const uint32_t* key_idx,
                        const uint32_t* pks, uint8_t* ct, uint64_t stride, MsgKey* keys,
-                       uint32_t* err, hipStream_t s);
+                       uint32_t* err, uint32_t* gate, uint32_t gate_val, hipStream_t s);
 // Open setup: epk from header, X25519 with the recipient secret key.
 void launch_open_setup(int M, const uint32_t* key_idx, const uint32_t* sks, const uint32_t* pks,
                        const uint8_t* ct, uint64_t stride, MsgKey* keys, uint32_t* err,
-                       hipStream_t s);
+                       uint32_t* gate, uint32_t gate_val, hipStream_t s);
+// Dispatch gate: the setup kernels store gate_val to *gate (if non-null) when
+// their first workgroup starts; k_gate_wait (one wave) polls for it, giving up
+// after timeout_us. Orders a side-stream setup's dispatch before a main-stream
+// grid launched right after it.
+void launch_gate_wait(const uint32_t* gate, uint32_t val, uint32_t timeout_us, hipStream_t s);
 // Standalone batched X25519 (tests / key generation): out[i] = X25519(sc[i], u[i]).
 void launch_x25519(int N, const uint32_t* scalars, const uint32_t* points, uint32_t* out,
                    hipStream_t s);
@@ -101,8 +106,10 @@ void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
                            uint64_t stride, hipStream_t s);
 // Poly1305 chunk partials (and, when decrypt!=0, in-place decryption plus
 // varint-terminator counts per chunk).
-void launch_mac_chunks(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,
-                       const uint32_t* pt_len, uint32_t* partials, int decrypt,
+// Per-message Poly1305 chunk factors r^(4(255-t)), t = 0..255: pows [M][256][5].
+void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s);
+void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,
+                       uint64_t stride, const uint32_t* pt_len, uint32_t* partials, int decrypt,
                        uint32_t* term_cnt, hipStream_t s);
 // Combine partials -> tag; mode 0 = write the header mac, 1 = verify (ok[j]).
 void launch_mac_final(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,

@@ -11,6 +11,30 @@
 namespace sdagpu {
 namespace {
 
+// ---- dispatch gate -----------------------------------------------------------
+// The X25519 setup kernels need ~150 VGPRs per wave. Launched on the side stream
+// at the same moment as a full-chip main-stream grid (the share kernel fills
+// every SIMD's register file), their workgroups only become resident once that
+// grid drains, and the first encrypt then waits on them (measured: 0.9 ms alone,
+// 4.9 ms next to the share kernel). So the setup kernel's first lane posts a
+// token when it is dispatched, and the main stream runs `k_gate_wait` -- one
+// wave polling the token, bounded by a timeout -- before its big grid: the
+// setup waves are resident first and run concurrently at their own latency.
+SDA_DEV void signal_dispatched(uint32_t* gate, uint32_t val) {
+  if (gate != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(gate, val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(64) k_gate_wait(const uint32_t* gate, uint32_t val,
+                                                  uint64_t timeout_ticks) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = wall_clock64();  // constant-rate (100 MHz) counter
+  while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != val) {
+    if (wall_clock64() - t0 > timeout_ticks) break;  // never wait unboundedly
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 SDA_DEV void derive_msg_key(MsgKey& out, const uint32_t (&shared)[8], const uint32_t (&epk)[8],
                             const uint32_t (&pk)[8]) {
   const uint32_t zero4[4] = {0, 0, 0, 0};
@@ -43,7 +67,13 @@ SDA_DEV void derive_msg_key(MsgKey& out, const uint32_t (&shared)[8], const uint
 __global__ void __launch_bounds__(64) k_seal_setup(int M, RngKeyArg rng, uint64_t owner_base,
                                                    const uint32_t* __restrict__ key_idx,
                                                    const uint32_t* __restrict__ pks, uint8_t* ct,
-                                                   uint64_t stride, MsgKey* keys, uint32_t* err) {
+                                                   uint64_t stride, MsgKey* keys, uint32_t* err,
+                                                   uint32_t* gate, uint32_t gate_val) {
+  signal_dispatched(gate, gate_val);
+  // Latency-bound ladders sharing SIMDs with the main stream's full-chip grids:
+  // top wave priority, so the arbiter issues them first and they finish at
+  // close to their stand-alone latency (the first encrypt waits on them).
+  __builtin_amdgcn_s_setprio(3);
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int j = t >> 1, role = t & 1;
   const bool live = j < M;
@@ -87,7 +117,10 @@ __global__ void __launch_bounds__(64) k_open_setup(int M, const uint32_t* __rest
                                                    const uint32_t* __restrict__ sks,
                                                    const uint32_t* __restrict__ pks,
                                                    const uint8_t* ct, uint64_t stride,
-                                                   MsgKey* keys, uint32_t* err) {
+                                                   MsgKey* keys, uint32_t* err,
+                                                   uint32_t* gate, uint32_t gate_val) {
+  signal_dispatched(gate, gate_val);
+  __builtin_amdgcn_s_setprio(3);  // see k_seal_setup
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= M) return;
   const uint32_t* hdr = reinterpret_cast<const uint32_t*>(ct + (size_t)j * stride);
@@ -126,19 +159,24 @@ __global__ void __launch_bounds__(64) k_x25519(int N, const uint32_t* __restrict
 
 void launch_seal_setup(int M, RngKeyArg rng, uint64_t owner_base, const uint32_t* key_idx,
                        const uint32_t* pks, uint8_t* ct, uint64_t stride, MsgKey* keys,
-                       uint32_t* err, hipStream_t s) {
+                       uint32_t* err, uint32_t* gate, uint32_t gate_val, hipStream_t s) {
   if (M <= 0) return;
   const int64_t threads = 2 * (int64_t)M;
   hipLaunchKernelGGL(k_seal_setup, dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, s, M, rng,
-                     owner_base, key_idx, pks, ct, stride, keys, err);
+                     owner_base, key_idx, pks, ct, stride, keys, err, gate, gate_val);
 }
 
 void launch_open_setup(int M, const uint32_t* key_idx, const uint32_t* sks, const uint32_t* pks,
                        const uint8_t* ct, uint64_t stride, MsgKey* keys, uint32_t* err,
-                       hipStream_t s) {
+                       uint32_t* gate, uint32_t gate_val, hipStream_t s) {
   if (M <= 0) return;
   hipLaunchKernelGGL(k_open_setup, dim3((M + 63) / 64), dim3(64), 0, s, M, key_idx, sks, pks, ct,
-                     stride, keys, err);
+                     stride, keys, err, gate, gate_val);
+}
+
+void launch_gate_wait(const uint32_t* gate, uint32_t val, uint32_t timeout_us, hipStream_t s) {
+  hipLaunchKernelGGL(k_gate_wait, dim3(1), dim3(64), 0, s, gate, val,
+                     (uint64_t)timeout_us * 100);
 }
 
 void launch_x25519(int N, const uint32_t* scalars, const uint32_t* points, uint32_t* out,

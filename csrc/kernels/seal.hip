@@ -182,17 +182,41 @@ SDA_DEV P130 load_block(const uint8_t* lds, int64_t i, int64_t kC, uint32_t N) {
   return p130_block(w[0], w[1], w[2], w[3], hibit);
 }
 
+// r^(4 * (255 - t)) for t = 0..255, per message: the factor that places lane t's
+// 4-block Horner sum at its distance from the chunk end. Computed once per
+// message (it depends only on the key), so a chunk's combine is one multiply
+// per lane plus a sum -- instead of an 8-level multiply tree per chunk.
+__global__ void __launch_bounds__(kBlock)
+    k_poly_powers(const MsgKey* __restrict__ keys, uint32_t* __restrict__ pows) {
+  __builtin_amdgcn_s_setprio(3);  // side-stream key work (see k_seal_setup)
+  const int j = blockIdx.x, t = threadIdx.x;
+  const MsgKey key = keys[j];
+  const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
+  const P130 r = p130_r_from_key(rk);
+  P130 r4 = p130_mul(r, r);
+  r4 = p130_mul(r4, r4);
+  const P130 f = p130_carry(p130_pow(r4, (uint32_t)(kBlock - 1 - t)));
+  uint32_t* o = pows + ((size_t)j * kBlock + t) * 5;
+#pragma unroll
+  for (int u = 0; u < 5; ++u) o[u] = f.v[u];
+}
+
+SDA_DEV uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
 template <int DECRYPT>
 __global__ void __launch_bounds__(kBlock)
-    k_mac_chunks(const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct, uint64_t stride,
-                 const uint32_t* __restrict__ pt_len, uint32_t* __restrict__ partials,
-                 uint32_t* __restrict__ term_cnt) {
+    k_mac_chunks(const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
+                 uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
+                 uint32_t* __restrict__ partials, uint32_t* __restrict__ term_cnt) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kChunkBytes];
-  __shared__ uint32_t tree[5][kBlock];
-  __shared__ uint32_t rpow[8][5];
+  __shared__ uint64_t lsum[5][kWaves];
   __shared__ uint32_t scratch[kWaves];
   const int k = blockIdx.x, j = blockIdx.y, K = gridDim.x;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint32_t N = pt_len[j];
   const int64_t kC = (int64_t)k * kChunkBytes;
   const int64_t start = kC >= 32 ? kC - 32 : 0;
@@ -204,6 +228,9 @@ __global__ void __launch_bounds__(kBlock)
     return;
   }
   uint8_t* gmsg = ct + (size_t)j * stride + 48;
+  // this lane's chunk factor (independent of the data: issue the loads first)
+  const uint32_t* pf = pows + ((size_t)j * kBlock + tid) * 5;
+  const P130 f = P130{{pf[0], pf[1], pf[2], pf[3], pf[4]}};
   // load the chunk (16-byte pieces overlapping [start, end))
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -214,7 +241,8 @@ __global__ void __launch_bounds__(kBlock)
   }
   __syncthreads();
 
-  // ---- Poly1305 partial over blocks [fb, eb)
+  // ---- Poly1305 partial over blocks [fb, eb): lane t Horner-sums 4 blocks
+  // ending 4 * (255 - t) blocks before the chunk end, then scales by its factor
   const MsgKey key = keys[j];
   const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
   const P130 r = p130_r_from_key(rk);
@@ -228,37 +256,33 @@ __global__ void __launch_bounds__(kBlock)
     if (i >= fb) c = load_block(buf, i, kC, N);
     h = p130_mul(p130_add(h, c), r);
   }
-  // r^(4 * 2^l), l = 0..7, computed once per block (lane 0) into LDS
+  h = p130_mul(h, f);
+  // block-wide sum of the limbs (64-bit: 256 x 2^27 fits easily), then carry
+  uint64_t sv[5];
+#pragma unroll
+  for (int u = 0; u < 5; ++u) sv[u] = wave_sum64((uint64_t)h.v[u]);
+  if (lane == 0) {
+#pragma unroll
+    for (int u = 0; u < 5; ++u) lsum[u][wave] = sv[u];
+  }
+  __syncthreads();  // also orders every lane's MAC reads of buf before the in-place decrypt
   if (tid == 0) {
-    P130 R = p130_mul(r, r);
-    R = p130_mul(R, R);
+    uint64_t d[5];
 #pragma unroll
-    for (int l = 0; l < 8; ++l) {
+    for (int u = 0; u < 5; ++u) {
+      d[u] = 0;
 #pragma unroll
-      for (int u = 0; u < 5; ++u) rpow[l][u] = R.v[u];
-      R = p130_mul(R, R);
+      for (int w = 0; w < kWaves; ++w) d[u] += lsum[u][w];
     }
-  }
+    uint64_t c;
+    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+    c = d[1] >> 26; d[1] &= kM26; d[2] += c;
+    c = d[2] >> 26; d[2] &= kM26; d[3] += c;
+    c = d[3] >> 26; d[3] &= kM26; d[4] += c;
+    c = d[4] >> 26; d[4] &= kM26; d[0] += c * 5;
+    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
 #pragma unroll
-  for (int l = 0; l < 8; ++l) {
-    const int s = 1 << l;
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < 5; ++u) tree[u][tid] = h.v[u];
-    __syncthreads();
-    if ((tid & (2 * s - 1)) == 2 * s - 1) {
-      P130 left, R;
-#pragma unroll
-      for (int u = 0; u < 5; ++u) {
-        left.v[u] = tree[u][tid - s];
-        R.v[u] = rpow[l][u];
-      }
-      h = p130_carry(p130_add(p130_mul(left, R), h));
-    }
-  }
-  if (tid == kBlock - 1) {
-#pragma unroll
-    for (int u = 0; u < 5; ++u) part[u] = h.v[u];
+    for (int u = 0; u < 5; ++u) part[u] = (uint32_t)d[u];
   }
 
   if constexpr (DECRYPT) {
@@ -372,16 +396,21 @@ void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
                        (const uint32_t*)vals, tile_off, keys, ct, stride);
 }
 
-void launch_mac_chunks(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,
-                       const uint32_t* pt_len, uint32_t* partials, int decrypt,
+void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(k_poly_powers, dim3(M), dim3(kBlock), 0, s, keys, pows);
+}
+
+void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,
+                       uint64_t stride, const uint32_t* pt_len, uint32_t* partials, int decrypt,
                        uint32_t* term_cnt, hipStream_t s) {
   if (M <= 0 || K <= 0) return;
   dim3 grid(K, M);
   if (decrypt)
-    hipLaunchKernelGGL(k_mac_chunks<1>, grid, dim3(kBlock), 0, s, keys, ct, stride, pt_len,
+    hipLaunchKernelGGL(k_mac_chunks<1>, grid, dim3(kBlock), 0, s, keys, pows, ct, stride, pt_len,
                        partials, term_cnt);
   else
-    hipLaunchKernelGGL(k_mac_chunks<0>, grid, dim3(kBlock), 0, s, keys, ct, stride, pt_len,
+    hipLaunchKernelGGL(k_mac_chunks<0>, grid, dim3(kBlock), 0, s, keys, pows, ct, stride, pt_len,
                        partials, term_cnt);
 }
 

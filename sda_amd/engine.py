@@ -168,9 +168,20 @@ class DeviceAggregator:
             mask_cnt = None  # PSS batches do not align with mask tiles: recounted
         return shares, cnt, mask_vals, mask_cnt
 
+    def _gate_token(self):
+        """A fresh (tensor, value) dispatch token for a side-stream setup kernel
+        that a main-stream `gate_wait` orders ahead of the next big grid."""
+        if getattr(self, "_gate", None) is None:
+            self._gate = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._gate_val = 0
+        self._gate_val = (self._gate_val + 1) & 0x7FFFFFFF or 1
+        return self._gate, self._gate_val
+
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            # high priority: its kernels are latency-bound X25519 ladders with few
+            # waves, which must not queue behind the main stream's full-chip grids
+            self._side = torch.cuda.Stream(device=self.device, priority=-1)
         return self._side
 
     def _live(self, clerks):
@@ -208,7 +219,6 @@ class DeviceAggregator:
         err = self.new_error_word()
         marks: list = []
         self._mark(marks, "start")
-        rk = self.prepare_reveal(live, err)
         if router_for is not None and waves > 1:
             self._mark(marks, "participate")
             combined, mask_sum = self.participate_and_clerk_pipelined(
@@ -219,6 +229,10 @@ class DeviceAggregator:
             combined, mask_sum = self.participate_and_clerk(secrets, live, err,
                                                             owner_base=owner_base, router=router,
                                                             marks=marks)
+        # the recipient's key agreement queues on the side stream BEHIND the
+        # participants' and clerks' (needed last; ahead of them it delayed the
+        # first encrypt by the length of an X25519 ladder)
+        rk = self.prepare_reveal(live, err)
         if reducer is not None:
             combined, mask_sum = self.reduce_partials(combined, mask_sum, reducer, marks)
             if combined is None:
@@ -279,7 +293,6 @@ class DeviceAggregator:
         main = torch.cuda.current_stream(dev)
         side = self._side_stream()
         pks, sks = self.keys.pks, self.keys.sks
-        KB = G.MSGKEY_BYTES
 
         arena = Arena.empty(n * P, B, m, dev)
         inbox = Arena(arena.M, arena.L, arena.modulus, arena.stride, arena.K,
@@ -292,9 +305,10 @@ class DeviceAggregator:
             mask_arena = Arena.empty(P, spec.masking.seed_words, 0, dev)
         kidx_rcpt = torch.full((P,), n, dtype=torch.int32, device=dev)
 
+        gate = self._gate_token()
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            ks = seal_setup(arena, kidx, pks, rng_key, 0, err)
+            ks = seal_setup(arena, kidx, pks, rng_key, 0, err, gate=gate)
             ks_mask = ko_mask = None
             if mask_arena is not None:
                 ks_mask = seal_setup(mask_arena, kidx_rcpt, pks, rng_key, n * P, err)
@@ -345,20 +359,20 @@ class DeviceAggregator:
             handle.wait()
             main.wait_event(ev_open)
             box = inbox.slice(n * lo, n * Pw)
-            kw = ko[n * lo * KB:n * hi * KB]
+            kw = ko.slice(n * lo, n * Pw)
             if len(live) == n:
                 vals = open_data(box, kw, err, out_dtype=self.vdtype)
             else:
                 vals = torch.empty(len(live), Pw, B, dtype=self.vdtype, device=dev)
                 for i, c in enumerate(live):
-                    open_data(box.slice(c * Pw, Pw), kw[c * Pw * KB:(c + 1) * Pw * KB], err,
+                    open_data(box.slice(c * Pw, Pw), kw.slice(c * Pw, Pw), err,
                               out=vals[i])
             comb = torch.empty(len(live), B, dtype=torch.int32, device=dev)
             G.colsum(vals.view(len(live), Pw, B), m, comb)
             acc = comb if acc is None else acc + comb
             if mask_arena is not None:
                 msum = torch.empty(D, dtype=torch.int32, device=dev)
-                mvals = open_data(mask_arena.slice(lo, Pw), ko_mask[lo * KB:hi * KB], err,
+                mvals = open_data(mask_arena.slice(lo, Pw), ko_mask.slice(lo, Pw), err,
                                   out_dtype=torch.int32)
                 if isinstance(spec.masking, FullMask):
                     G.colsum(mvals.view(1, Pw, D), m, msum)
@@ -367,16 +381,17 @@ class DeviceAggregator:
                 macc = msum if macc is None else macc + msum
 
         ko = ev_open = None
+        G.gate_wait(gate)
         for lo, hi in bounds:
             Pw = hi - lo
             shares, cnt, mvals, mcnt = self._share(secrets[lo:hi], rng_key, owner_base + lo, err)
             if ko is None:  # the first wave's shares overlap the whole-round seal setup
                 ko, ev_open = start_headers()
             box = arena.slice(n * lo, n * Pw)
-            seal_data(box, ks[n * lo * KB:n * hi * KB], shares.view(n * Pw, B), err, cnt)
+            seal_data(box, ks.slice(n * lo, n * Pw), shares.view(n * Pw, B), err, cnt)
             del shares
             if mask_arena is not None:
-                seal_data(mask_arena.slice(lo, Pw), ks_mask[lo * KB:hi * KB], mvals, err, mcnt)
+                seal_data(mask_arena.slice(lo, Pw), ks_mask.slice(lo, Pw), mvals, err, mcnt)
             _, handle = router_for(Pw).exchange_async(box, inbox=inbox.slice(n * lo, n * Pw))
             if pending is not None:
                 finish(pending)
@@ -421,9 +436,10 @@ class DeviceAggregator:
         kidx_rcpt_p = torch.full((P,), n, dtype=torch.int32, device=dev)
 
         # ---- side stream: key agreement (data independent)
+        gate = self._gate_token()
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            ks_clerk = seal_setup(clerk_arena, kidx_clerk, pks, rng_key, 0, err)
+            ks_clerk = seal_setup(clerk_arena, kidx_clerk, pks, rng_key, 0, err, gate=gate)
             ks_mask = (seal_setup(mask_arena, kidx_rcpt_p, pks, rng_key, n * P, err)
                        if mask_arena is not None else None)
             ev_sealkeys = torch.cuda.Event()
@@ -439,6 +455,7 @@ class DeviceAggregator:
                 t.record_stream(main)
 
         # ---- participants: mask + share, then encrypt (waits for the seal keys)
+        G.gate_wait(gate)  # the setup waves are resident before the share grid
         shares, cnt, mask_vals, mask_cnt = self._share(secrets, rng_key, owner_base, err)
         main.wait_event(ev_sealkeys)
         seal_data(clerk_arena, ks_clerk, shares.view(n * P, B), err, cnt)
@@ -514,17 +531,18 @@ class DeviceAggregator:
         rng_key = native().crypto.random_bytes(32)
         main = torch.cuda.current_stream(dev)
         side = self._side_stream()
-        res_arena = Arena.empty(len(live), self.spec.batches, m, dev)
-        kidx = torch.full((len(live),), n, dtype=torch.int32, device=dev)
-        side.wait_stream(main)
+        # Everything is allocated on the side stream and nothing here waits for
+        # the main stream: called after the round's participant/clerk work has
+        # been queued, it must not serialise behind it. (`err` and the key
+        # tensors are long-lived; `err` is only OR-ed into.)
         with torch.cuda.stream(side):
+            res_arena = Arena.empty(len(live), self.spec.batches, m, dev)
+            kidx = torch.full((len(live),), n, dtype=torch.int32, device=dev)
             ks = seal_setup(res_arena, kidx, pks, rng_key, 0, err)
             ko = open_setup(res_arena, kidx, sks, pks, err)
             ev = torch.cuda.Event()
             ev.record(side)
-        for t in (res_arena.ct, res_arena.pt_len, kidx):  # main-stream tensors used on side
-            t.record_stream(side)
-        for t in (ks, ko):  # side-stream tensors consumed on main
+        for t in (res_arena.ct, res_arena.pt_len, ks, ko):  # side-stream tensors used on main
             t.record_stream(main)
         return res_arena, ks, ko, ev
 
@@ -533,7 +551,10 @@ class DeviceAggregator:
         reconstructs (sum / Lagrange over the live clerks) and unmasks."""
         spec, n, m = self.spec, self.n, self.m
         B, D, dev = spec.batches, spec.dimension, self.device
-        res_arena, ks_res, ko_res, ev = keys if keys is not None else self.prepare_reveal(live, err)
+        if keys is None:  # not prepared ahead: order after this round's main work (err init)
+            self._side_stream().wait_stream(torch.cuda.current_stream(dev))
+            keys = self.prepare_reveal(live, err)
+        res_arena, ks_res, ko_res, ev = keys
         torch.cuda.current_stream(dev).wait_event(ev)
         res_vals = combined if self.vdtype == torch.int32 else combined.to(self.vdtype)
         seal_data(res_arena, ks_res, res_vals, err)

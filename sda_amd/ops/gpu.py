@@ -13,6 +13,7 @@ from .._native import gpu as _gpu
 TILE_VALUES = 4096
 CHUNK_BYTES = 16384
 MSGKEY_BYTES = 80
+POW_WORDS = 256 * 5  # Poly1305 chunk factors per message (k_poly_powers)
 SEAL_OVERHEAD = 48
 
 MASK_NONE, MASK_FULL, MASK_CHACHA = 0, 1, 2
@@ -77,7 +78,16 @@ def rng_words(key: bytes) -> list[int]:
 
 
 # --------------------------------------------------------------- launches ----
-def seal_setup(M, rng_key, owner_base, key_idx, pks, ct, stride, keys, err):
+def _gate_args(gate):
+    """(tensor, value) dispatch token or None -> (pointer, value)."""
+    if gate is None:
+        return 0, 0
+    t, v = gate
+    _check(t, "gate", torch.int32, numel=1)
+    return _ptr(t), int(v) & 0xFFFFFFFF
+
+
+def seal_setup(M, rng_key, owner_base, key_idx, pks, ct, stride, keys, err, gate=None):
     _check(key_idx, "key_idx", torch.int32, numel=M)
     _check(pks, "pks", torch.int32)
     if pks.numel() % 8:
@@ -88,10 +98,10 @@ def seal_setup(M, rng_key, owner_base, key_idx, pks, ct, stride, keys, err):
     if stride % 64:
         raise ValueError("stride must be a multiple of 64")
     _gpu().seal_setup(M, rng_words(rng_key), owner_base, _ptr(key_idx), _ptr(pks), _ptr(ct),
-                      stride, _ptr(keys), _ptr(err), _stream())
+                      stride, _ptr(keys), _ptr(err), *_gate_args(gate), _stream())
 
 
-def open_setup(M, key_idx, sks, pks, ct, stride, keys, err):
+def open_setup(M, key_idx, sks, pks, ct, stride, keys, err, gate=None):
     _check(key_idx, "key_idx", torch.int32, numel=M)
     _check(sks, "sks", torch.int32)
     _check(pks, "pks", torch.int32, numel=sks.numel())
@@ -99,7 +109,14 @@ def open_setup(M, key_idx, sks, pks, ct, stride, keys, err):
     _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
     _check(err, "err", torch.int32, numel=1)
     _gpu().open_setup(M, _ptr(key_idx), _ptr(sks), _ptr(pks), _ptr(ct), stride, _ptr(keys),
-                      _ptr(err), _stream())
+                      _ptr(err), *_gate_args(gate), _stream())
+
+
+def gate_wait(gate, timeout_us: int = 3000):
+    """On the current stream: wait (bounded) until a setup kernel launched with
+    `gate` has been dispatched (see launch_gate_wait)."""
+    ptr, val = _gate_args(gate)
+    _gpu().gate_wait(ptr, val, int(timeout_us), _stream())
 
 
 def x25519(scalars: torch.Tensor, points: torch.Tensor) -> torch.Tensor:
@@ -214,14 +231,21 @@ def encode_encrypt(vals, tile_off, keys, ct, stride):
                           _ptr(ct), stride, _stream())
 
 
-def mac_chunks(M, K, keys, ct, stride, pt_len, partials, decrypt, term_cnt=None):
+def poly_powers(M, keys, pows):
     _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
+    _check(pows, "pows", torch.int32, min_numel=M * POW_WORDS)
+    _gpu().poly_powers(M, _ptr(keys), _ptr(pows), _stream())
+
+
+def mac_chunks(M, K, keys, pows, ct, stride, pt_len, partials, decrypt, term_cnt=None):
+    _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
+    _check(pows, "pows", torch.int32, min_numel=M * POW_WORDS)
     _check(ct, "ct", torch.uint8, min_numel=M * stride)
     _check(pt_len, "pt_len", torch.int32, numel=M)
     _check(partials, "partials", torch.int32, numel=M * K * 8)
     if decrypt:
         _check(term_cnt, "term_cnt", torch.int32, numel=M * K)
-    _gpu().mac_chunks(M, K, _ptr(keys), _ptr(ct), stride, _ptr(pt_len), _ptr(partials),
+    _gpu().mac_chunks(M, K, _ptr(keys), _ptr(pows), _ptr(ct), stride, _ptr(pt_len), _ptr(partials),
                       1 if decrypt else 0, _ptr(term_cnt) if term_cnt is not None else 0, _stream())
 
 

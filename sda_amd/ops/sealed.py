@@ -81,19 +81,60 @@ class Arena:
                      self.pt_len[first:first + count])
 
 
+@dataclass
+class KeySet:
+    """Per-message derived keys: the 80-byte `MsgKey` records (XSalsa20 subkey,
+    nonce tail, Poly1305 r/s) and each message's Poly1305 chunk-factor table
+    r^(4(255-t)), t < 256 (5 x 26-bit limbs), which lets `k_mac_chunks` combine
+    a 16 KiB chunk with one multiply per lane. Both depend only on the key
+    agreement, so they are produced together on the side stream."""
+    M: int
+    keys: torch.Tensor  # uint8 [M * MSGKEY_BYTES]
+    pows: torch.Tensor | None  # int32 [M * POW_WORDS]; None = not derived yet
+
+    @classmethod
+    def derive(cls, M: int, keys: torch.Tensor) -> "KeySet":
+        return cls(M, keys, None).with_powers()
+
+    def with_powers(self) -> "KeySet":
+        """The chunk-factor table (on the current stream) if not derived yet."""
+        if self.pows is not None:
+            return self
+        pows = torch.empty(self.M * G.POW_WORDS, dtype=torch.int32, device=self.keys.device)
+        G.poly_powers(self.M, self.keys, pows)
+        return KeySet(self.M, self.keys, pows)
+
+    def slice(self, first: int, count: int) -> "KeySet":
+        """Keys of messages [first, first+count) (no copy)."""
+        if first < 0 or first + count > self.M:
+            raise ValueError("key slice out of range")
+        kb, pw = G.MSGKEY_BYTES, G.POW_WORDS
+        return KeySet(count, self.keys[first * kb:(first + count) * kb],
+                      None if self.pows is None else self.pows[first * pw:(first + count) * pw])
+
+    def record_stream(self, stream) -> None:
+        self.keys.record_stream(stream)
+        if self.pows is not None:
+            self.pows.record_stream(stream)
+
+
 def seal_setup(arena: Arena, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: bytes,
-               owner_base: int, err: torch.Tensor) -> torch.Tensor:
+               owner_base: int, err: torch.Tensor, gate=None) -> KeySet:
     """Ephemeral keypairs + X25519 + nonce/subkey derivation for every slot.
 
     Independent of the message contents, so the engine runs it on a side stream
     concurrently with share generation. Writes epk into each slot header.
+    The Poly1305 chunk factors are left to :func:`seal_data` (a 30 us kernel on
+    the consuming stream), so the encrypt waits on the X25519 work only.
+    `gate`: (int32 tensor, token) posted when the kernel is dispatched.
     """
     keys = torch.empty(arena.M * G.MSGKEY_BYTES, dtype=torch.uint8, device=arena.ct.device)
-    G.seal_setup(arena.M, rng_key, owner_base, key_idx, pks, arena.ct, arena.stride, keys, err)
-    return keys
+    G.seal_setup(arena.M, rng_key, owner_base, key_idx, pks, arena.ct, arena.stride, keys, err,
+                 gate=gate)
+    return KeySet(arena.M, keys, None)
 
 
-def seal_data(arena: Arena, keys: torch.Tensor, values: torch.Tensor, err: torch.Tensor,
+def seal_data(arena: Arena, keys: KeySet, values: torch.Tensor, err: torch.Tensor,
               cnt: torch.Tensor | None = None) -> Arena:
     """Varint-encode + encrypt + MAC the rows of `values` [M][L] into `arena`."""
     M, L = values.shape
@@ -106,11 +147,15 @@ def seal_data(arena: Arena, keys: torch.Tensor, values: torch.Tensor, err: torch
         G.count(values, cnt)
     else:
         cnt = cnt.view(M, T)
+    if keys.M != M:
+        raise ValueError("key set does not match the arena")
     G.segscan(cnt, arena.pt_len)  # cnt becomes the tile byte offsets
-    G.encode_encrypt(values, cnt, keys, arena.ct, arena.stride)
+    G.encode_encrypt(values, cnt, keys.keys, arena.ct, arena.stride)
+    keys = keys.with_powers()
     partials = torch.empty(M * arena.K * 8, dtype=torch.int32, device=dev)
-    G.mac_chunks(M, arena.K, keys, arena.ct, arena.stride, arena.pt_len, partials, decrypt=False)
-    G.mac_final(M, arena.K, keys, arena.ct, arena.stride, arena.pt_len, partials, verify=False,
+    G.mac_chunks(M, arena.K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
+                 decrypt=False)
+    G.mac_final(M, arena.K, keys.keys, arena.ct, arena.stride, arena.pt_len, partials, verify=False,
                 err=err)
     return arena
 
@@ -127,14 +172,14 @@ def seal(values: torch.Tensor, key_idx: torch.Tensor, pks: torch.Tensor, rng_key
 
 
 def open_setup(arena: Arena, key_idx: torch.Tensor, sks: torch.Tensor, pks: torch.Tensor,
-               err: torch.Tensor) -> torch.Tensor:
+               err: torch.Tensor, gate=None) -> KeySet:
     """X25519(sk, epk) + derivations for every slot (needs only the headers)."""
     keys = torch.empty(arena.M * G.MSGKEY_BYTES, dtype=torch.uint8, device=arena.ct.device)
-    G.open_setup(arena.M, key_idx, sks, pks, arena.ct, arena.stride, keys, err)
-    return keys
+    G.open_setup(arena.M, key_idx, sks, pks, arena.ct, arena.stride, keys, err, gate=gate)
+    return KeySet.derive(arena.M, keys)
 
 
-def open_data(arena: Arena, keys: torch.Tensor, err: torch.Tensor,
+def open_data(arena: Arena, keys: KeySet, err: torch.Tensor,
               out_dtype: torch.dtype | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """Verify + decrypt (in place) + decode every message; returns [M][L] values.
 
@@ -142,11 +187,13 @@ def open_data(arena: Arena, keys: torch.Tensor, err: torch.Tensor,
     """
     M, L, K = arena.M, arena.L, arena.K
     dev = arena.ct.device
+    if keys.M != M:
+        raise ValueError("key set does not match the arena")
     partials = torch.empty(M * K * 8, dtype=torch.int32, device=dev)
     term = torch.empty(M, K, dtype=torch.int32, device=dev)
-    G.mac_chunks(M, K, keys, arena.ct, arena.stride, arena.pt_len, partials, decrypt=True,
-                 term_cnt=term)
-    G.mac_final(M, K, keys, arena.ct, arena.stride, arena.pt_len, partials, verify=True, err=err)
+    G.mac_chunks(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
+                 decrypt=True, term_cnt=term)
+    G.mac_final(M, K, keys.keys, arena.ct, arena.stride, arena.pt_len, partials, verify=True, err=err)
     totals = torch.empty(M, dtype=torch.int32, device=dev)
     G.segscan(term, totals)
     # exactly L values per message, otherwise malformed

@@ -108,7 +108,7 @@ class StreamingAggregator:
         err = eng.new_error_word()
         marks: list = []
         eng._mark(marks, "start")
-        rk = eng.prepare_reveal(live, err)
+        rk = None  # recipient key agreement: queued behind the first wave's
         done = 0
         for w in range(start, waves):
             first = w * self.wave
@@ -124,6 +124,8 @@ class StreamingAggregator:
                 comb, msum = eng.participate_and_clerk(x, live, err,
                                                        owner_base=owner_base + first,
                                                        router=router)
+            if rk is None:
+                rk = eng.prepare_reveal(live, err)
             acc += comb
             if mask_acc is not None:
                 mask_acc += msum
