@@ -141,10 +141,10 @@ PYBIND11_MODULE(_sda_gpu, m) {
   });
   m.def("mac_chunks", [](int M, int K, uintptr_t keys, uintptr_t pows, uintptr_t ct,
                          uint64_t stride, uintptr_t pt_len, uintptr_t partials, int decrypt,
-                         uintptr_t term_cnt, uintptr_t stream) {
+                         uintptr_t term_cnt, uintptr_t sub_cnt, uintptr_t stream) {
     launch_mac_chunks(M, K, P<const MsgKey>(keys), P<const uint32_t>(pows), P<uint8_t>(ct), stride,
                       P<const uint32_t>(pt_len), P<uint32_t>(partials), decrypt,
-                      P<uint32_t>(term_cnt), S(stream));
+                      P<uint32_t>(term_cnt), P<uint32_t>(sub_cnt), S(stream));
     check_launch("mac_chunks");
   });
   m.def("mac_final", [](int M, int K, uintptr_t keys, uintptr_t ct, uint64_t stride,
@@ -162,6 +162,25 @@ PYBIND11_MODULE(_sda_gpu, m) {
                   P<const uint32_t>(pt_len), P<const uint32_t>(elem_start), P<void>(vals),
                   P<uint32_t>(err), S(stream));
     check_launch("decode");
+  });
+  m.attr("SUB_BYTES") = kSubBytes;
+  m.attr("SUM_TILE") = kSumTile;
+  m.def("locate_tiles", [](int M, int Sn, int L, uintptr_t pre, uintptr_t totals,
+                           uintptr_t tile_sub, uintptr_t stream) {
+    launch_locate_tiles(M, Sn, L, P<const uint32_t>(pre), P<const uint32_t>(totals),
+                        P<uint32_t>(tile_sub), S(stream));
+    check_launch("locate_tiles");
+  });
+  m.def("decode_sum", [](int R, int Pn, int Pg, int L, uint32_t mod, uintptr_t pt, uint64_t stride,
+                         uintptr_t pt_len, int Sn, uintptr_t pre, uintptr_t tile_sub,
+                         uintptr_t part, uintptr_t out, uintptr_t err, uintptr_t stream) {
+    if (mod == 0) throw std::invalid_argument("decode_sum: needs a modulus");
+    if ((uint64_t)Pg * (mod - 1) > 0xffffffffull)
+      throw std::invalid_argument("decode_sum: Pg * (m - 1) overflows the u32 accumulators");
+    launch_decode_sum(R, Pn, Pg, L, mod, P<const uint8_t>(pt), stride, P<const uint32_t>(pt_len), Sn,
+                      P<const uint32_t>(pre), P<const uint32_t>(tile_sub), P<uint32_t>(part),
+                      P<uint32_t>(out), P<uint32_t>(err), S(stream));
+    check_launch("decode_sum");
   });
   m.def("colsum", [](int G, int R, int L, uint32_t mod, int value_bytes, uintptr_t vals,
                      uintptr_t out, uintptr_t stream) {

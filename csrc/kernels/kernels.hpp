@@ -31,6 +31,9 @@ static_assert(sizeof(MsgKey) == 80, "MsgKey layout");
 constexpr int kTileValues = 4096;    // values per byte-count tile (256 lanes x 16)
 constexpr int kEncodeValues = 8192;  // values per encode tile = 2 count tiles (256 x 32)
 constexpr int kChunkBytes = 16384;  // bytes per MAC / decrypt chunk (256 threads x 64)
+constexpr int kSubBytes = 1024;     // terminator-count granularity (16 lanes x 64 B)
+constexpr int kSubPerChunk = kChunkBytes / kSubBytes;
+constexpr int kSumTile = 6144;      // elements per decode-sum tile (~11 KiB of varints at m = 433)
 
 // Error bits (device error word)
 enum ErrBits : uint32_t {
@@ -108,9 +111,11 @@ void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
 // varint-terminator counts per chunk).
 // Per-message Poly1305 chunk factors r^(4(255-t)), t = 0..255: pows [M][256][5].
 void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s);
+// With decrypt, term_cnt [M][K] (per chunk) and/or sub_cnt [M][K * kSubPerChunk]
+// (per 1 KiB sub-chunk) receive terminator counts (either may be null).
 void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,
                        uint64_t stride, const uint32_t* pt_len, uint32_t* partials, int decrypt,
-                       uint32_t* term_cnt, hipStream_t s);
+                       uint32_t* term_cnt, uint32_t* sub_cnt, hipStream_t s);
 // Combine partials -> tag; mode 0 = write the header mac, 1 = verify (ok[j]).
 void launch_mac_final(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,
                       const uint32_t* pt_len, const uint32_t* partials, int verify,
@@ -121,6 +126,16 @@ void launch_mac_final(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t st
 void launch_decode(int M, int K, int L, uint32_t m, int value_bytes, const uint8_t* pt,
                    uint64_t stride, const uint32_t* pt_len, const uint32_t* elem_start,
                    void* vals, uint32_t* err, hipStream_t s);
+// Fused clerk decode + combine over rows R (clerks) x P participants, message
+// j = r * P + p. pre [M][S] = exclusive sub-chunk terminator ranks (segscan of
+// sub_cnt), totals [M]; tile_sub [M][T+1] scratch (T = ceil(L / kSumTile));
+// part [G][R][L] scratch slabs (G = ceil(P / Pg); needs Pg * (m - 1) < 2^32);
+// out [R][L] = sum_p values mod m.
+void launch_locate_tiles(int M, int S, int L, const uint32_t* pre, const uint32_t* totals,
+                         uint32_t* tile_sub, hipStream_t s);
+void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* pt, uint64_t stride,
+                       const uint32_t* pt_len, int S, const uint32_t* pre, const uint32_t* tile_sub,
+                       uint32_t* part, uint32_t* out, uint32_t* err, hipStream_t s);
 // Column sums mod m: out[g][l] = sum_r vals[g][r][l] mod m.
 void launch_colsum(int G, int R, int L, uint32_t m, int value_bytes, const void* vals,
                    uint32_t* out, hipStream_t s);

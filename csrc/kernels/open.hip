@@ -12,6 +12,7 @@
 // varints ending in its 64 bytes, reading at most 9 bytes back (a 16-byte LDS
 // prefix of the previous chunk covers varints straddling the boundary).
 #include "block_utils.hpp"
+#include "decode_core.hpp"
 #include "device_crypto.hpp"
 #include "kernels.hpp"
 #include "modarith.hpp"
@@ -19,50 +20,24 @@
 namespace sdagpu {
 namespace {
 
-// Canonical field value of a decoded zigzag varint (general path handles
-// negative / oversized values from foreign encoders such as the reference's
-// Rust-`%` shares, which can be negative: additive.rs:47).
-SDA_DEV uint32_t canon_varint(uint64_t z, const ModParams& mp, bool& bad) {
-  if (!(z & 1)) {
-    const uint64_t mag = z >> 1;
-    if (mp.m == 0) {
-      bad |= mag > 0xffffffffULL;
-      return (uint32_t)mag;
-    }
-    return mag < mp.m ? (uint32_t)mag : mod64(mag, mp);
+// Sink of k_decode: the chunk's values staged in LDS at their block-local rank
+// (non-terminators into a per-lane dummy slot).
+template <typename VT>
+struct StageSink {
+  static constexpr bool kAdditive = false;
+  VT* outb;
+  uint32_t dummy;
+  SDA_DEV void put(uint32_t local, uint32_t v, uint32_t term) {
+    outb[term ? local : dummy] = (VT)v;
   }
-  if (mp.m == 0) {
-    bad = true;
-    return 0;
-  }
-  const uint32_t r = mod64((z >> 1) + 1, mp);  // value = -(z>>1) - 1
-  return r == 0 ? 0u : mp.m - r;
-}
-
-typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
-
-// Two candidate values from a word holding two (previous byte, byte) pairs in
-// its 16-bit halves: z = prev-is-continuation ? byte<<7 | prev&0x7f : byte,
-// then zigzag-decode and reduce a value in (-m, m) into [0, m). Halves whose
-// byte is not a terminator produce garbage the caller discards.
-SDA_DEV uint32_t pair_values(uint32_t P, u16x2 mpair) {
-  const uint32_t z2 = ((P >> 1) & 0x7f807f80u) | (P & 0x007f007fu);
-  const uint32_t z1 = (P >> 8) & 0x00ff00ffu;
-  const uint32_t sel = ((P >> 7) & 0x00010001u) * 0xffffu;
-  const uint32_t z = (sel & z2) | (~sel & z1);
-  const uint32_t neg = z & 0x00010001u;
-  const uint32_t u = ((z >> 1) & 0x7fff7fffu) + neg;  // |value|, no carry across halves
-  const uint32_t nsel = neg * 0xffffu;
-  const uint32_t mu = __builtin_bit_cast(uint32_t, mpair - __builtin_bit_cast(u16x2, u));
-  return (nsel & mu) | (~nsel & u);
-}
+  SDA_DEV void put_rank(uint32_t rank, uint32_t v) { outb[rank] = (VT)v; }
+};
 
 // One block per (chunk, message). Each lane owns 64 plaintext bytes held in
 // registers; terminator positions are a 64-bit mask (popcount -> block scan ->
 // ranks); the bytes preceding a lane come from its neighbour by a shuffle (lane
 // 0 of a wave loads them); decoded values are staged in LDS so the global store
-// of the chunk's contiguous element range is coalesced. Varints of 3+ bytes
-// (large moduli, ChaCha seeds) walk back through global memory.
+// of the chunk's contiguous element range is coalesced.
 template <typename VT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
     k_decode(int L, ModParams mp, const uint8_t* __restrict__ pt, uint64_t stride,
@@ -80,145 +55,19 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   const uint8_t* gmsg = pt + (size_t)j * stride + 48;
   const int64_t p0 = kC - 32 + 64 * tid;  // message position of this lane's first byte
   uint32_t w[16];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t pos = p0 + 16 * q;
-    uint4 d = make_uint4(0, 0, 0, 0);
-    if (pos >= 0 && pos < end) d = *reinterpret_cast<const uint4*>(gmsg + pos);
-    w[4 * q] = d.x; w[4 * q + 1] = d.y; w[4 * q + 2] = d.z; w[4 * q + 3] = d.w;
-  }
-  // the 4 bytes before this lane's range, for lane 0 of each wave (the other
-  // lanes take them from their neighbour below)
+  load_lane_bytes(w, gmsg, p0, end);
   uint32_t wave_prev = 0;
   if ((tid & 63) == 0 && p0 - 4 >= 0 && p0 - 4 < end) wave_prev = *reinterpret_cast<const uint32_t*>(gmsg + p0 - 4);
-  // valid bytes [lo, hi) of this lane
   const int lo = (int)max((int64_t)0, start - p0);
   const int hi = (int)min((int64_t)64, end - p0);
-  uint64_t vmask = 0;
-  if (hi > lo) {
-    const uint64_t upto = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
-    vmask = upto & ~((1ull << lo) - 1);
-  }
-  uint64_t tmask = 0;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const uint32_t t = ~w[i] & 0x80808080u;
-    const uint64_t bits = ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
-    tmask |= bits << (4 * i);
-  }
-  const uint64_t traw = tmask;
-  tmask &= vmask;
+  const uint64_t traw = term_mask64(w);
+  const uint64_t tmask = traw & byte_range_mask(lo, hi);
   uint32_t total;
-  uint32_t local = block_excl_scan((uint32_t)__popcll(tmask), scratch, &total);  // syncs
-  bool bad = false;
-  // The two bytes preceding this lane's range (previous lane's last word; lane 0
-  // of each wave reads them from the LDS image, which holds the chunk prefix).
+  const uint32_t local = block_excl_scan((uint32_t)__popcll(tmask), scratch, &total);  // syncs
   uint32_t prev_word = __shfl_up(w[15], 1, 64);
   if ((tid & 63) == 0) prev_word = wave_prev;
-  // Fast path (u16 values, modulus < 2^16, no varint longer than two bytes,
-  // canonical range): SWAR over 16-bit halves -- one 32-bit op yields the
-  // candidate values of two byte positions. Odd positions pair with the byte
-  // before them inside the same half of the word; even positions use the word
-  // realigned by one byte (v_alignbyte). Every position then stores its
-  // candidate, non-terminators into a per-lane dummy slot. A lane that meets a
-  // longer varint or an out-of-range value re-runs the generic path below.
-  const uint32_t local0 = local;
-  const uint32_t dummy = kChunkBytes + 2 * (tid & 63);  // own dword per lane of a wave
-  const uint32_t tmask_lo = (uint32_t)tmask, tmask_hi = (uint32_t)(tmask >> 32);
-  bool redo = true;
-  if constexpr (sizeof(VT) == 2) {
-    if (mp.m != 0 && mp.m < 65536u) {
-      const uint64_t craw = ~traw;  // continuation bytes
-      const uint32_t cm1 = prev_word >> 31, cm2 = (prev_word >> 23) & 1u;
-      const bool longv = (craw & (craw << 1)) != 0 || (cm1 & ((uint32_t)craw & 1u)) || (cm1 & cm2);
-      const u16x2 mpair = {(uint16_t)mp.m, (uint16_t)mp.m};
-      u16x2 vmax = {0, 0};
-      uint32_t wp = prev_word;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t W = w[i];
-        const uint32_t Pe = __builtin_amdgcn_alignbyte(W, wp, 3);  // [wp.B3 W.B0 | W.B1 W.B2]
-        const uint32_t ve = pair_values(Pe, mpair), vo = pair_values(W, mpair);
-        const uint32_t t4 = ((i < 8 ? tmask_lo : tmask_hi) >> (4 * (i & 7))) & 15u;
-        const uint32_t te = ((t4 & 1u) * 0xffffu) | (((t4 >> 2) & 1u) * 0xffff0000u);
-        const uint32_t to = (((t4 >> 1) & 1u) * 0xffffu) | (((t4 >> 3) & 1u) * 0xffff0000u);
-        vmax = __builtin_elementwise_max(vmax, __builtin_bit_cast(u16x2, ve & te));
-        vmax = __builtin_elementwise_max(vmax, __builtin_bit_cast(u16x2, vo & to));
-        uint32_t t;
-        t = t4 & 1u;        outb[t ? local : dummy] = (VT)ve;         local += t;
-        t = (t4 >> 1) & 1u; outb[t ? local : dummy] = (VT)vo;         local += t;
-        t = (t4 >> 2) & 1u; outb[t ? local : dummy] = (VT)(ve >> 16); local += t;
-        t = (t4 >> 3) & 1u; outb[t ? local : dummy] = (VT)(vo >> 16); local += t;
-        wp = W;
-      }
-      redo = longv || vmax.x >= mp.m || vmax.y >= mp.m;
-    }
-  }
-  if (redo) {
-    // Generic path, all in registers (the LDS image is only touched by the
-    // rare long-varint walk: lanes 64 B apart would all hit the same two LDS
-    // banks). A terminator at b closes a 1-, 2- or 3-byte varint depending on
-    // the continuation bits of bytes b-1, b-2; four bytes and more
-    // (|value| >= 2^20) take the LDS walk.
-    // opaque copies: stop the compiler from sharing (and keeping live across
-    // the fast path) the per-byte terms it would otherwise CSE between paths
-    uint32_t tlo = tmask_lo, thi = tmask_hi;
-    local = local0;
-    asm volatile("" : "+v"(tlo), "+v"(thi), "+v"(local));
-    uint32_t long_mask_lo = 0, long_mask_hi = 0;  // terminators needing the slow path
-    uint32_t b3 = (prev_word >> 8) & 0xffu, b2 = (prev_word >> 16) & 0xffu, b1 = prev_word >> 24;
-    // Branch-free: every byte stores a value, non-terminators into a per-lane
-    // dummy slot, so the unrolled loop compiles to straight-line VALU + ds_write.
-    // Conditions are kept as integer 0/1 / all-ones masks (bools become SGPR
-    // lane masks that the compiler then spills across the unrolled loop).
-    uint32_t neg_raw = 0;
-  #pragma unroll
-    for (int b = 0; b < 64; ++b) {
-      const uint32_t byte = (w[b >> 2] >> (8 * (b & 3))) & 0xffu;
-      const uint32_t term = ((b < 32 ? tlo : thi) >> (b & 31)) & 1u;
-      const uint32_t c1 = b1 >> 7, c2 = b2 >> 7, c3 = b3 >> 7;
-      const uint32_t m1 = 0u - c1, m2 = 0u - c2;
-      const uint32_t z2 = (b1 & 0x7f) | (byte << 7);
-      const uint32_t z3 = (b2 & 0x7f) | ((b1 & 0x7f) << 7) | (byte << 14);
-      const uint32_t z = (byte & ~m1) | (z2 & m1 & ~m2) | (z3 & m1 & m2);  // < 2^21
-      const uint32_t lng = term & c1 & c2 & c3;
-      if (b < 32) long_mask_lo |= lng << b; else long_mask_hi |= lng << (b - 32);
-      const uint32_t neg = z & 1u;
-      const uint32_t u = (z >> 1) + neg;  // |value| (value = -u when neg)
-      const uint32_t r = mod32(u, mp);    // m == 0: raw
-      const uint32_t nr = r == 0 ? 0u : mp.m - r;
-      const uint32_t v = r ^ ((r ^ nr) & (0u - neg));
-      neg_raw |= term & neg & (lng ^ 1u);
-      const uint32_t addr = dummy ^ ((dummy ^ local) & (0u - term));
-      outb[addr] = (VT)v;
-      local += term;
-      b3 = b2;
-      b2 = b1;
-      b1 = byte;
-    }
-    if (mp.m == 0) bad |= neg_raw != 0;  // a raw (modulus-free) stream holds no negatives
-    // rare slow path: rewrite the values of >= 3-byte varints
-    uint64_t lm = ((uint64_t)long_mask_hi << 32) | long_mask_lo;
-    if (lm) {
-      uint32_t rank0 = local - (uint32_t)__popcll(tmask);
-      while (lm) {
-        const int b = __builtin_ctzll(lm);
-        lm &= lm - 1;
-        const uint32_t r = rank0 + (uint32_t)__popcll(tmask & ((1ull << b) - 1));
-        const int64_t q = p0 + b;
-        int64_t s0 = q;
-        int n = 0;
-        while (n < 10 && s0 > 0 && (gmsg[s0 - 1] & 0x80)) { --s0; ++n; }
-        bad |= n >= 10;
-        uint64_t z = 0;
-        for (int64_t u = s0; u <= q; ++u) {
-          const uint32_t sh = 7u * (uint32_t)(u - s0);
-          if (sh < 64) z |= (uint64_t)(gmsg[u] & 0x7f) << sh;
-        }
-        outb[r] = (VT)canon_varint(z, mp, bad);
-      }
-    }
-  }
+  StageSink<VT> sink{outb, (uint32_t)(kChunkBytes + 2 * (tid & 63))};
+  bool bad = decode_lane<sizeof(VT) == 2>(w, prev_word, tmask, traw, local, mp, gmsg, p0, sink);
   // a message must end on a terminator
   if (hi > lo && p0 + hi == (int64_t)N && (gmsg[N - 1] & 0x80)) bad = true;
   __syncthreads();
@@ -229,6 +78,157 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     else bad = true;
   }
   if (bad) atomicOr(err, kErrMalformed);
+}
+
+// ---------------------------------------------------- clerk decode + combine
+// The clerk's combine (sharing/combiner.rs:15-29: element-wise sum over the P
+// participants' share vectors) fused with the varint decode, so decoded shares
+// never reach HBM. Element tiles are aligned across participants: block (t, r,
+// g) owns elements [t*kSumTile, (t+1)*kSumTile) of row r (a clerk) and walks
+// participant group g. k_mac_chunks<1> counts terminators per 1 KiB sub-chunk,
+// their exclusive scan gives each sub-chunk's first rank, and k_locate_tiles
+// records per (message, tile) the sub-chunk holding the tile's first
+// terminator, so a block reads only the ~kSumTile * 1.9 bytes of each message
+// that hold its tile (plus < 2 KiB of sub-chunk slack). Values are accumulated
+// with LDS atomics (ds_add_u32) into a kSumTile-wide u32 accumulator; each
+// group writes a slab of raw sums, and k_sum_slabs reduces the slabs mod m.
+// The accumulator has kSumMargin slots on both sides of the tile: a pass's
+// ranks lie within one 1 KiB sub-chunk (< 1024 terminators) of the tile on
+// either side, so every rank lands in [0, kSumTile + 2 * kSumMargin] with no
+// bounds check, and a non-terminator adds 0 to the next rank's slot.
+constexpr int kSumMargin = kSubBytes;
+constexpr int kSumAcc = kSumTile + 2 * kSumMargin + 64;
+struct AddSink {
+  static constexpr bool kAdditive = true;
+  uint32_t* acc;  // acc[kSumMargin] = tile element 0
+  uint32_t off;   // accumulator index of block-local rank 0
+  SDA_DEV void put(uint32_t local, uint32_t v, uint32_t term) {
+    atomicAdd(acc + (local + off), v & (0u - term));
+  }
+  SDA_DEV void put_masked(uint32_t local, uint32_t v) { atomicAdd(acc + (local + off), v); }
+  SDA_DEV void put_rank(uint32_t rank, uint32_t v) { atomicAdd(acc + (rank + off), v); }
+};
+
+__global__ void __launch_bounds__(kBlock)
+    k_locate_tiles(int S, int T, const uint32_t* __restrict__ pre,
+                   const uint32_t* __restrict__ totals, uint32_t* __restrict__ tile_sub) {
+  const int s = blockIdx.x * kBlock + threadIdx.x, j = blockIdx.y;
+  if (s >= S) return;
+  const uint32_t tot = totals[j];
+  const uint32_t lo = pre[(size_t)j * S + s];
+  const uint32_t hi = s + 1 < S ? pre[(size_t)j * S + s + 1] : tot;
+  uint32_t* row = tile_sub + (size_t)j * (T + 1);
+  // tiles whose first element ends in this sub-chunk (a 1 KiB sub-chunk holds
+  // < kSumTile terminators: at most one)
+  for (uint32_t t = (lo + kSumTile - 1) / kSumTile; t <= (uint32_t)T && (uint64_t)t * kSumTile < hi; ++t)
+    row[t] = (uint32_t)s;
+  // tiles past the message's last element (t = T always: the end sentinel)
+  if (s == S - 1)
+    for (uint64_t t = ((uint64_t)tot + kSumTile - 1) / kSumTile; t <= (uint64_t)T; ++t) row[t] = (uint32_t)S;
+}
+
+// Each wave walks its own participants (round-robin over the group) in 4 KiB
+// passes -- 64 lanes x 64 bytes, ranks by a wave scan -- so no block barrier
+// sits between a pass's loads and the next: 16 independent waves per CU keep
+// their loads in flight. The waves share the tile accumulator through ds_add.
+template <bool kFast16, typename Sink>
+SDA_DEV void decode_sum_body(uint32_t* acc, uint32_t (*info)[4], int L, int P, int Pg,
+                             const ModParams& mp, const uint8_t* __restrict__ pt, uint64_t stride,
+                             const uint32_t* __restrict__ pt_len, int S,
+                             const uint32_t* __restrict__ pre, const uint32_t* __restrict__ tile_sub,
+                             uint32_t* __restrict__ part, uint32_t* err) {
+  constexpr int kWaveBytes = 64 * 64;
+  const int t = blockIdx.x, r = blockIdx.y, g = blockIdx.z, R = gridDim.y;
+  const int T = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t E0 = (uint32_t)t * kSumTile;
+  const uint32_t W = min((uint32_t)kSumTile, (uint32_t)L - E0);
+  for (int i = tid; i < kSumAcc; i += kBlock) acc[i] = 0;
+  const int pbeg = g * Pg, pend = min(P, pbeg + Pg);
+  bool bad = false;
+  for (int b0 = pbeg; b0 < pend; b0 += kBlock) {
+    const int cnt = min(kBlock, pend - b0);
+    __syncthreads();  // previous batch's info reads done (and acc zeroed)
+    if (tid < cnt) {
+      const size_t j = (size_t)r * P + b0 + tid;
+      const uint32_t s0 = tile_sub[j * (T + 1) + t];
+      info[tid][0] = s0;
+      info[tid][1] = tile_sub[j * (T + 1) + t + 1];
+      info[tid][2] = s0 < (uint32_t)S ? pre[j * S + s0] : 0u;
+      info[tid][3] = pt_len[j];
+    }
+    __syncthreads();
+    for (int i = wave; i < cnt; i += kWaves) {
+      const uint32_t s0 = info[i][0];
+      if (s0 >= (uint32_t)S) continue;  // fewer elements than the tile start: malformed, flagged by the totals
+      const uint32_t s1 = min(info[i][1], (uint32_t)S - 1);
+      const int64_t N = info[i][3];
+      const uint8_t* gmsg = pt + ((size_t)r * P + b0 + i) * stride + 48;
+      const int64_t qs = max((int64_t)0, (int64_t)s0 * kSubBytes - 32);
+      const int64_t qe = min(N, ((int64_t)s1 + 1) * kSubBytes - 32);
+      uint32_t rank = info[i][2];
+      for (int64_t c0 = (int64_t)s0 * kSubBytes - 32; c0 < qe; c0 += kWaveBytes) {
+        const int64_t p0 = c0 + 64 * lane;
+        uint32_t w[16];
+        load_lane_bytes(w, gmsg, p0, qe);
+        uint32_t wave_prev = 0;
+        if (lane == 0 && p0 - 4 >= 0 && p0 - 4 < N) wave_prev = *reinterpret_cast<const uint32_t*>(gmsg + p0 - 4);
+        const int lo = (int)max((int64_t)0, qs - p0);
+        const int hi = (int)min((int64_t)64, qe - p0);
+        const uint64_t traw = term_mask64(w);
+        const uint64_t tmask = traw & byte_range_mask(lo, hi);
+        const uint32_t c = (uint32_t)__popcll(tmask);
+        const uint32_t incl = wave_incl_scan(c);
+        const uint32_t total = __shfl(incl, 63, 64);
+        uint32_t prev_word = __shfl_up(w[15], 1, 64);
+        if (lane == 0) prev_word = wave_prev;
+        Sink sink{acc, rank + kSumMargin - E0};
+        bad |= decode_lane<kFast16>(w, prev_word, tmask, traw, incl - c, mp, gmsg, p0, sink);
+        if (hi > lo && p0 + hi == N && (gmsg[N - 1] & 0x80)) bad = true;
+        rank += total;
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t* out = part + ((size_t)g * R + r) * L + E0;
+  for (uint32_t i = tid; i < W; i += kBlock) out[i] = acc[kSumMargin + i];
+  if (bad) atomicOr(err, kErrMalformed);
+}
+
+// No occupancy hint: the unrolled decode paths need ~200 VGPRs (2 waves per
+// SIMD); squeezing them into 128 or 168 spilled and measured slower.
+template <bool kFast16>
+__global__ void __launch_bounds__(kBlock)
+    k_decode_sum(int L, int P, int Pg, ModParams mp, const uint8_t* __restrict__ pt,
+                 uint64_t stride, const uint32_t* __restrict__ pt_len, int S,
+                 const uint32_t* __restrict__ pre, const uint32_t* __restrict__ tile_sub,
+                 uint32_t* __restrict__ part, uint32_t* err) {
+  __shared__ uint32_t acc[kSumAcc];
+  __shared__ uint32_t info[kBlock][4];
+  decode_sum_body<kFast16, AddSink>(acc, info, L, P, Pg, mp, pt, stride, pt_len, S, pre, tile_sub,
+                                    part, err);
+}
+
+// out[x] = sum_g part[g][x] mod m   (x < X = rows * L)
+__global__ void __launch_bounds__(kBlock)
+    k_sum_slabs(int G, int64_t X, ModParams mp, const uint32_t* __restrict__ part,
+                uint32_t* __restrict__ out) {
+  const int64_t x = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+  if (x >= X) return;
+  if (x + 4 <= X && (X % 4) == 0) {
+    uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    for (int g = 0; g < G; ++g) {
+      const uint4 q = *reinterpret_cast<const uint4*>(part + g * X + x);
+      a0 += q.x; a1 += q.y; a2 += q.z; a3 += q.w;
+    }
+    *reinterpret_cast<uint4*>(out + x) = make_uint4(mod64(a0, mp), mod64(a1, mp), mod64(a2, mp), mod64(a3, mp));
+  } else {
+    for (int64_t y = x; y < min(X, x + 4); ++y) {
+      uint64_t a = 0;
+      for (int g = 0; g < G; ++g) a += part[g * X + y];
+      out[y] = mod64(a, mp);
+    }
+  }
 }
 
 template <typename VT, typename ACC>
@@ -306,6 +306,34 @@ void launch_decode(int M, int K, int L, uint32_t m, int value_bytes, const uint8
   else
     hipLaunchKernelGGL(k_decode<uint32_t>, grid, dim3(kBlock), 0, s, L, mp, pt, stride, pt_len,
                        elem_start, (uint32_t*)vals, err);
+}
+
+void launch_locate_tiles(int M, int S, int L, const uint32_t* pre, const uint32_t* totals,
+                         uint32_t* tile_sub, hipStream_t s) {
+  if (M <= 0 || S <= 0 || L <= 0) return;
+  const int T = (L + kSumTile - 1) / kSumTile;
+  hipLaunchKernelGGL(k_locate_tiles, dim3((S + kBlock - 1) / kBlock, M), dim3(kBlock), 0, s, S, T,
+                     pre, totals, tile_sub);
+}
+
+void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* pt, uint64_t stride,
+                       const uint32_t* pt_len, int S, const uint32_t* pre, const uint32_t* tile_sub,
+                       uint32_t* part, uint32_t* out, uint32_t* err, hipStream_t s) {
+  if (R <= 0 || P <= 0 || L <= 0 || Pg <= 0 || m == 0) return;
+  const ModParams mp = make_mod_params(m);
+  const int T = (L + kSumTile - 1) / kSumTile;
+  const int G = (P + Pg - 1) / Pg;
+  dim3 grid(T, R, G);
+  if (m < 65536u)
+    hipLaunchKernelGGL(k_decode_sum<true>, grid, dim3(kBlock), 0, s, L, P, Pg, mp, pt, stride,
+                       pt_len, S, pre, tile_sub, part, err);
+  else
+    hipLaunchKernelGGL(k_decode_sum<false>, grid, dim3(kBlock), 0, s, L, P, Pg, mp, pt, stride,
+                       pt_len, S, pre, tile_sub, part, err);
+  const int64_t X = (int64_t)R * L;
+  const int64_t threads = (X + 3) / 4;
+  hipLaunchKernelGGL(k_sum_slabs, dim3((unsigned)((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                     G, X, mp, part, out);
 }
 
 void launch_colsum(int G, int R, int L, uint32_t m, int value_bytes, const void* vals,

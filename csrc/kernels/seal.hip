@@ -211,7 +211,8 @@ template <int DECRYPT>
 __global__ void __launch_bounds__(kBlock)
     k_mac_chunks(const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
                  uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
-                 uint32_t* __restrict__ partials, uint32_t* __restrict__ term_cnt) {
+                 uint32_t* __restrict__ partials, uint32_t* __restrict__ term_cnt,
+                 uint32_t* __restrict__ sub_cnt) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kChunkBytes];
   __shared__ uint64_t lsum[5][kWaves];
   __shared__ uint32_t scratch[kWaves];
@@ -224,7 +225,9 @@ __global__ void __launch_bounds__(kBlock)
   uint32_t* part = partials + ((size_t)j * K + k) * 8;
   if (start >= end) {  // chunk beyond the message (or empty message)
     if (tid < 5) part[tid] = 0;
-    if (DECRYPT && tid == 0) term_cnt[(size_t)j * K + k] = 0;
+    if (DECRYPT && term_cnt && tid == 0) term_cnt[(size_t)j * K + k] = 0;
+    if (DECRYPT && sub_cnt && tid < kSubPerChunk)
+      sub_cnt[((size_t)j * K + k) * kSubPerChunk + tid] = 0;
     return;
   }
   uint8_t* gmsg = ct + (size_t)j * stride + 48;
@@ -319,8 +322,16 @@ __global__ void __launch_bounds__(kBlock)
       }
     }
     const uint32_t cnt = (uint32_t)__popcll(tmask & vmask);
-    const uint32_t tot = block_sum(cnt, scratch);
-    if (tid == 0) term_cnt[(size_t)j * K + k] = tot;
+    if (sub_cnt) {  // per 1 KiB sub-chunk: the 16 lanes covering it
+      uint32_t sc = cnt;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) sc += __shfl_xor(sc, o, 64);
+      if ((tid & 15) == 0) sub_cnt[((size_t)j * K + k) * kSubPerChunk + (tid >> 4)] = sc;
+    }
+    if (term_cnt) {
+      const uint32_t tot = block_sum(cnt, scratch);
+      if (tid == 0) term_cnt[(size_t)j * K + k] = tot;
+    }
     // store plaintext in place (bytes past `end` land in the slot padding)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -403,15 +414,15 @@ void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s
 
 void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,
                        uint64_t stride, const uint32_t* pt_len, uint32_t* partials, int decrypt,
-                       uint32_t* term_cnt, hipStream_t s) {
+                       uint32_t* term_cnt, uint32_t* sub_cnt, hipStream_t s) {
   if (M <= 0 || K <= 0) return;
   dim3 grid(K, M);
   if (decrypt)
     hipLaunchKernelGGL(k_mac_chunks<1>, grid, dim3(kBlock), 0, s, keys, pows, ct, stride, pt_len,
-                       partials, term_cnt);
+                       partials, term_cnt, sub_cnt);
   else
     hipLaunchKernelGGL(k_mac_chunks<0>, grid, dim3(kBlock), 0, s, keys, pows, ct, stride, pt_len,
-                       partials, term_cnt);
+                       partials, term_cnt, sub_cnt);
 }
 
 void launch_mac_final(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,

@@ -1,9 +1,7 @@
-# quick iteration: new/changed GPU tests first, then the full GPU suite, bench, kernel stats
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
-T=${GPU_TESTS:-tests}
-timeout -k 10 600 python -u -m pytest $T -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 --stages > gpurun_out/bench.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 > gpurun_out/prof_bench.log 2>&1

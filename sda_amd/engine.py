@@ -28,7 +28,8 @@ import torch
 from ._native import native
 from .models.schemes import Additive, AggregationSpec, ChaChaMask, FullMask, PackedShamir
 from .ops import gpu as G
-from .ops.sealed import Arena, open_, open_data, open_setup, seal, seal_data, seal_setup
+from .ops.sealed import (Arena, open_, open_data, open_setup, open_sum, seal, seal_data,
+                         seal_setup)
 from .utils.trace import tracing_enabled
 
 _TRACE = tracing_enabled()
@@ -358,26 +359,11 @@ class DeviceAggregator:
             Pw = hi - lo
             handle.wait()
             main.wait_event(ev_open)
-            box = inbox.slice(n * lo, n * Pw)
-            kw = ko.slice(n * lo, n * Pw)
-            if len(live) == n:
-                vals = open_data(box, kw, err, out_dtype=self.vdtype)
-            else:
-                vals = torch.empty(len(live), Pw, B, dtype=self.vdtype, device=dev)
-                for i, c in enumerate(live):
-                    open_data(box.slice(c * Pw, Pw), kw.slice(c * Pw, Pw), err,
-                              out=vals[i])
-            comb = torch.empty(len(live), B, dtype=torch.int32, device=dev)
-            G.colsum(vals.view(len(live), Pw, B), m, comb)
+            comb = self._open_combine(inbox.slice(n * lo, n * Pw), ko.slice(n * lo, n * Pw),
+                                      live, Pw, err)
             acc = comb if acc is None else acc + comb
             if mask_arena is not None:
-                msum = torch.empty(D, dtype=torch.int32, device=dev)
-                mvals = open_data(mask_arena.slice(lo, Pw), ko_mask.slice(lo, Pw), err,
-                                  out_dtype=torch.int32)
-                if isinstance(spec.masking, FullMask):
-                    G.colsum(mvals.view(1, Pw, D), m, msum)
-                else:
-                    G.chacha_mask_sum(mvals, D, m, msum, err)
+                msum = self._open_masks(mask_arena.slice(lo, Pw), ko_mask.slice(lo, Pw), err)
                 macc = msum if macc is None else macc + msum
 
         ko = ev_open = None
@@ -472,34 +458,47 @@ class DeviceAggregator:
 
     def _clerk(self, st, live, err):
         """Open + combine an inbox (the local arena or the routed one)."""
-        spec, n, m = self.spec, self.n, self.m
-        P, B, D, dev = st["P"], spec.batches, spec.dimension, self.device
-        main = torch.cuda.current_stream(dev)
+        P = st["P"]
+        main = torch.cuda.current_stream(self.device)
         main.wait_event(st["ev_openkeys"])
         inbox = st.pop("inbox")
         ko_clerk = st.get("ko_clerk") or self._open_keys(inbox, st["kidx"], live, P, err)
-        if len(live) == n:
-            vals = open_data(inbox, ko_clerk[0], err, out_dtype=self.vdtype)
-        else:
-            vals = torch.empty(len(live), P, B, dtype=self.vdtype, device=dev)
-            for i, c in enumerate(live):
-                open_data(inbox.slice(c * P, P), ko_clerk[i], err, out=vals[i])
+        combined = self._open_combine(inbox, ko_clerk, live, P, err)
         del inbox
-        combined = torch.empty(len(live), B, dtype=torch.int32, device=dev)
-        G.colsum(vals.view(len(live), P, B), m, combined)
-        del vals
         # recipient's share of the mask work is data-parallel too: open these
         # participants' mask boxes and sum them
         mask_sum = None
         mask_arena = st["mask_arena"]
         if mask_arena is not None:
-            mask_sum = torch.empty(D, dtype=torch.int32, device=dev)
-            mvals = open_data(mask_arena, st["ko_mask"], err, out_dtype=torch.int32)
-            if isinstance(spec.masking, FullMask):
-                G.colsum(mvals.view(1, P, D), m, mask_sum)
-            else:
-                G.chacha_mask_sum(mvals, D, m, mask_sum, err)
+            mask_sum = self._open_masks(mask_arena, st["ko_mask"], err)
         return combined, mask_sum
+
+    def _open_combine(self, box: Arena, keys, live, P: int, err) -> torch.Tensor:
+        """The clerks' open + combine (clerk.rs:79-86) of a clerk-major inbox of
+        n x P boxes: [len(live)][B] int32 sums mod m, decode fused with the sum
+        (:func:`open_sum`). `keys`: one KeySet for all n x P boxes, or a list
+        with one per live clerk (``_open_keys``)."""
+        n = self.n
+        out = torch.empty(len(live), self.spec.batches, dtype=torch.int32, device=self.device)
+        if len(live) == n:
+            open_sum(box, keys[0] if isinstance(keys, list) else keys, err, rows=n, out=out)
+        else:
+            for i, c in enumerate(live):
+                kc = keys[i] if isinstance(keys, list) else keys.slice(c * P, P)
+                open_sum(box.slice(c * P, P), kc, err, rows=1, out=out[i])
+        return out
+
+    def _open_masks(self, mask_arena: Arena, keys, err) -> torch.Tensor:
+        """Recipient: open the participants' mask boxes and sum the masks
+        (full.rs:37-52) or re-expand and sum the ChaCha seeds (chacha.rs:56-77)."""
+        D, m = self.spec.dimension, self.m
+        mask_sum = torch.empty(D, dtype=torch.int32, device=self.device)
+        if isinstance(self.spec.masking, FullMask):
+            open_sum(mask_arena, keys, err, rows=1, out=mask_sum)
+        else:
+            seeds = open_data(mask_arena, keys, err, out_dtype=torch.int32)
+            G.chacha_mask_sum(seeds, D, m, mask_sum, err)
+        return mask_sum
 
     def reduce_partials(self, combined, mask_sum, reducer, marks=None):
         """Bucket the clerk rows (B wide) and the mask row (D wide) into one
@@ -558,17 +557,18 @@ class DeviceAggregator:
         torch.cuda.current_stream(dev).wait_event(ev)
         res_vals = combined if self.vdtype == torch.int32 else combined.to(self.vdtype)
         seal_data(res_arena, ks_res, res_vals, err)
-        ys = open_data(res_arena, ko_res, err, out_dtype=torch.int32)
         masked = torch.empty(D, dtype=torch.int32, device=dev)
-        if self._pss is None:
-            G.colsum(ys.view(1, n, B), m, masked)
-        elif self._pss_mfma:
-            lag_limbs, kp = self._lagrange_limbs(live)
-            G.modgemm_i8(lag_limbs, G.limbs_t(ys, kp, self._limbs), m, masked, ldc_z=0, ldc_m=1,
-                         ldc_n=spec.sharing.secret_count, limit=D)
+        if self._pss is None:  # additive: the reconstruction is the sum of the n results
+            open_sum(res_arena, ko_res, err, rows=1, out=masked)
         else:
-            lag = self._lagrange(live)
-            G.pss_reconstruct(ys, lag, spec.sharing.secret_count, D, m, masked)
+            ys = open_data(res_arena, ko_res, err, out_dtype=torch.int32)
+            if self._pss_mfma:
+                lag_limbs, kp = self._lagrange_limbs(live)
+                G.modgemm_i8(lag_limbs, G.limbs_t(ys, kp, self._limbs), m, masked, ldc_z=0,
+                             ldc_m=1, ldc_n=spec.sharing.secret_count, limit=D)
+            else:
+                lag = self._lagrange(live)
+                G.pss_reconstruct(ys, lag, spec.sharing.secret_count, D, m, masked)
         out = masked
         if mask_sum is not None:
             out = torch.empty(D, dtype=torch.int32, device=dev)

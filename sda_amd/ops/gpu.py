@@ -12,6 +12,9 @@ from .._native import gpu as _gpu
 
 TILE_VALUES = 4096
 CHUNK_BYTES = 16384
+SUB_BYTES = 1024                  # terminator-count granularity of the fused clerk path
+SUB_PER_CHUNK = CHUNK_BYTES // SUB_BYTES
+SUM_TILE = 6144                   # elements per decode-sum tile (k_decode_sum)
 MSGKEY_BYTES = 80
 POW_WORDS = 256 * 5  # Poly1305 chunk factors per message (k_poly_powers)
 SEAL_OVERHEAD = 48
@@ -237,16 +240,26 @@ def poly_powers(M, keys, pows):
     _gpu().poly_powers(M, _ptr(keys), _ptr(pows), _stream())
 
 
-def mac_chunks(M, K, keys, pows, ct, stride, pt_len, partials, decrypt, term_cnt=None):
+def mac_chunks(M, K, keys, pows, ct, stride, pt_len, partials, decrypt, term_cnt=None,
+               sub_cnt=None):
+    """Poly1305 chunk partials; with `decrypt`, in-place decryption plus varint
+    terminator counts per 16 KiB chunk (`term_cnt` [M][K]) and/or per 1 KiB
+    sub-chunk (`sub_cnt` [M][K * SUB_PER_CHUNK])."""
     _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
     _check(pows, "pows", torch.int32, min_numel=M * POW_WORDS)
     _check(ct, "ct", torch.uint8, min_numel=M * stride)
     _check(pt_len, "pt_len", torch.int32, numel=M)
     _check(partials, "partials", torch.int32, numel=M * K * 8)
     if decrypt:
-        _check(term_cnt, "term_cnt", torch.int32, numel=M * K)
+        if term_cnt is None and sub_cnt is None:
+            raise ValueError("decrypt needs term_cnt and/or sub_cnt")
+        if term_cnt is not None:
+            _check(term_cnt, "term_cnt", torch.int32, numel=M * K)
+        if sub_cnt is not None:
+            _check(sub_cnt, "sub_cnt", torch.int32, numel=M * K * SUB_PER_CHUNK)
     _gpu().mac_chunks(M, K, _ptr(keys), _ptr(pows), _ptr(ct), stride, _ptr(pt_len), _ptr(partials),
-                      1 if decrypt else 0, _ptr(term_cnt) if term_cnt is not None else 0, _stream())
+                      1 if decrypt else 0, _ptr(term_cnt) if term_cnt is not None else 0,
+                      _ptr(sub_cnt) if sub_cnt is not None else 0, _stream())
 
 
 def mac_final(M, K, keys, ct, stride, pt_len, partials, verify, ok=None, err=None):
@@ -264,6 +277,42 @@ def decode(M, K, L, modulus, pt, stride, pt_len, elem_start, vals, err):
     _check(pt, "pt", torch.uint8, min_numel=M * stride)
     _gpu().decode(M, K, L, modulus, value_bytes(vals.dtype), _ptr(pt), stride, _ptr(pt_len),
                   _ptr(elem_start), _ptr(vals), _ptr(err), _stream())
+
+
+def sum_tiles(L: int) -> int:
+    return (L + SUM_TILE - 1) // SUM_TILE
+
+
+def locate_tiles(pre: torch.Tensor, totals: torch.Tensor, L: int, tile_sub: torch.Tensor):
+    """tile_sub[j][t] = the sub-chunk holding the terminator of element t*SUM_TILE
+    of message j (end sentinel S past the message), from the exclusive
+    sub-chunk ranks `pre` [M][S]."""
+    M, S = pre.shape
+    _check(pre, "pre", torch.int32)
+    _check(totals, "totals", torch.int32, numel=M)
+    _check(tile_sub, "tile_sub", torch.int32, numel=M * (sum_tiles(L) + 1))
+    _gpu().locate_tiles(M, S, L, _ptr(pre), _ptr(totals), _ptr(tile_sub), _stream())
+
+
+def decode_sum(rows: int, P: int, Pg: int, L: int, modulus: int, pt, stride, pt_len, pre,
+               tile_sub, part, out, err):
+    """out[r] = sum_p decode(message r*P + p) mod m (fused decode + combine)."""
+    M = rows * P
+    S = pre.shape[1]
+    if modulus <= 0:
+        raise ValueError("decode_sum needs a modulus")
+    if Pg < 1 or Pg * (modulus - 1) >= 2 ** 32:
+        raise ValueError("decode_sum: Pg * (m - 1) must fit the u32 accumulators")
+    groups = (P + Pg - 1) // Pg
+    _check(pt, "pt", torch.uint8, min_numel=M * stride)
+    _check(pt_len, "pt_len", torch.int32, numel=M)
+    _check(pre, "pre", torch.int32, numel=M * S)
+    _check(tile_sub, "tile_sub", torch.int32, numel=M * (sum_tiles(L) + 1))
+    _check(part, "part", torch.int32, numel=groups * rows * L)
+    _check(out, "out", torch.int32, numel=rows * L)
+    _check(err, "err", torch.int32, numel=1)
+    _gpu().decode_sum(rows, P, Pg, L, modulus, _ptr(pt), stride, _ptr(pt_len), S, _ptr(pre),
+                      _ptr(tile_sub), _ptr(part), _ptr(out), _ptr(err), _stream())
 
 
 def colsum(vals: torch.Tensor, modulus: int, out: torch.Tensor):

@@ -14,6 +14,8 @@ bytes ``[0, 48 + pt_len[j])`` are a wire-format `Encryption` blob.
             encode + XSalsa20 -> parallel Poly1305 -> header tag
 ``open_`` : setup -> Poly1305 verify fused with in-place decryption and
             terminator counting -> element ranks -> parallel varint decode
+``open_sum``: the clerk's open + combine: as ``open_`` up to the terminator
+            counts (per 1 KiB), then decode fused with the sum over participants
 """
 from __future__ import annotations
 
@@ -201,6 +203,47 @@ def open_data(arena: Arena, keys: KeySet, err: torch.Tensor,
     if out is None:
         out = torch.empty(M, L, dtype=out_dtype or G.value_dtype(arena.modulus), device=dev)
     G.decode(M, K, L, arena.modulus, arena.ct, arena.stride, arena.pt_len, term, out, err)
+    return out
+
+
+def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
+             out: torch.Tensor) -> torch.Tensor:
+    """Verify + decrypt + decode + combine: out[r] = sum over p of the values of
+    message r * P + p, mod the arena modulus (P = M / rows).
+
+    The clerk's open-and-combine (reference clerk.rs:79-86) without
+    materialising decoded shares: the MAC pass counts varint terminators per
+    1 KiB sub-chunk, element tiles are located in every message, and
+    `k_decode_sum` accumulates each tile over all participants in LDS.
+    Destroys the ciphertext (it is replaced by plaintext).
+    """
+    M, L, K, m = arena.M, arena.L, arena.K, arena.modulus
+    if rows < 1 or M % rows:
+        raise ValueError("arena messages are not rows x participants")
+    if m <= 0:
+        raise ValueError("open_sum needs a modulus")
+    if keys.M != M:
+        raise ValueError("key set does not match the arena")
+    P = M // rows
+    dev = arena.ct.device
+    S = K * G.SUB_PER_CHUNK
+    partials = torch.empty(M * K * 8, dtype=torch.int32, device=dev)
+    pre = torch.empty(M, S, dtype=torch.int32, device=dev)
+    G.mac_chunks(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
+                 decrypt=True, sub_cnt=pre)
+    G.mac_final(M, K, keys.keys, arena.ct, arena.stride, arena.pt_len, partials, verify=True, err=err)
+    totals = torch.empty(M, dtype=torch.int32, device=dev)
+    G.segscan(pre, totals)  # sub-chunk counts -> exclusive ranks
+    err.bitwise_or_((totals != L).any().to(torch.int32) * 4)
+    T = G.sum_tiles(L)
+    tile_sub = torch.empty(M, T + 1, dtype=torch.int32, device=dev)
+    G.locate_tiles(pre, totals, L, tile_sub)
+    # participant groups: ~4k blocks fill the chip; u32 accumulators bound Pg
+    groups = max(1, min(P, -(-4096 // (T * rows))))
+    Pg = min(-(-P // groups), (2 ** 32 - 1) // max(1, m - 1))
+    part = torch.empty(-(-P // Pg), rows, L, dtype=torch.int32, device=dev)
+    G.decode_sum(rows, P, Pg, L, m, arena.ct, arena.stride, arena.pt_len, pre, tile_sub, part,
+                 out, err)
     return out
 
 

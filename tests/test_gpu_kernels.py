@@ -79,6 +79,79 @@ def test_host_seal_opens_on_gpu(cuda, native, L):
     assert out.cpu().tolist() == rows
 
 
+def _open_sum_case(native, cuda, rows_, P, L, m, gen):
+    """Host-sealed boxes (row-major: message r*P + p) -> open_sum vs a plain sum."""
+    from sda_amd.ops.sealed import Arena, open_setup, open_sum
+    keys = _keytable(native, cuda, 1)
+    vals, blobs = [], []
+    for j in range(rows_ * P):
+        row = gen(j)
+        vals.append([x % m for x in row])
+        blobs.append(native.crypto.box_seal(varint_encode(row), keys.pk_bytes[0]))
+    arena = Arena.from_blobs(blobs, L, m, cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    kidx = torch.zeros(rows_ * P, dtype=torch.int32, device=cuda)
+    ks = open_setup(arena, kidx, keys.sks, keys.pks, err)
+    out = torch.empty(rows_, L, dtype=torch.int32, device=cuda)
+    open_sum(arena, ks, err, rows=rows_, out=out)
+    ref = torch.tensor(vals, dtype=torch.int64).view(rows_, P, L).sum(1) % m
+    return int(err.item()), out.cpu().to(torch.int64), ref
+
+
+@pytest.mark.parametrize("L", [1, 7, 6144, 6145, 20000, 40000])
+def test_open_sum_matches_torch(cuda, native, L):
+    """Fused decode + combine over participants whose varint streams drift
+    apart (all-1-byte, all-2-byte and mixed rows, Rust-style negatives)."""
+    m = 433
+
+    def gen(j):
+        kind = j % 4
+        if kind == 0:
+            return [0] * L                                         # 1-byte varints
+        if kind == 1:
+            return torch.randint(200, m, (L,)).tolist()            # 2-byte varints
+        if kind == 2:
+            return torch.randint(-m + 1, m, (L,)).tolist()         # negatives (additive.rs:47)
+        return torch.randint(0, m, (L,)).tolist()
+    e, out, ref = _open_sum_case(native, cuda, 3, 9, L, m, gen)
+    assert e == 0
+    assert torch.equal(out, ref)
+
+
+def test_open_sum_foreign_encodings(cuda, native):
+    """Non-canonical values (>= m, long varints up to 10 bytes) take the generic
+    and slow decode paths inside the fused kernel; large modulus (u32 path)."""
+    L = 9000
+
+    def gen_small(j):
+        row = torch.randint(0, 433, (L,)).tolist()
+        for i in range(j, L, 97):
+            row[i] = [433 * 5 + 7, -(2 ** 40) - 3, 2 ** 62 + 11, 70000][i % 4]
+        return row
+    e, out, ref = _open_sum_case(native, cuda, 2, 5, L, 433, gen_small)
+    assert e == 0
+    assert torch.equal(out, ref)
+
+    big = 2 ** 31 - 1
+    e, out, ref = _open_sum_case(native, cuda, 1, 6, L, big,
+                                 lambda j: torch.randint(-big + 1, big, (L,)).tolist())
+    assert e == 0
+    assert torch.equal(out, ref)
+
+
+def test_open_sum_flags_wrong_length(cuda, native):
+    from sda_amd.ops.sealed import Arena, open_setup, open_sum
+    keys = _keytable(native, cuda, 1)
+    L = 5000
+    blobs = [native.crypto.box_seal(varint_encode(list(range(L - (j == 1)))), keys.pk_bytes[0])
+             for j in range(3)]
+    arena = Arena.from_blobs(blobs, L, 433, cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    ks = open_setup(arena, torch.zeros(3, dtype=torch.int32, device=cuda), keys.sks, keys.pks, err)
+    open_sum(arena, ks, err, rows=1, out=torch.empty(L, dtype=torch.int32, device=cuda))
+    assert int(err.item()) & 4
+
+
 def test_tampered_box_is_rejected(cuda, native):
     from sda_amd.ops.sealed import Arena, open_
     keys = _keytable(native, cuda, 1)
