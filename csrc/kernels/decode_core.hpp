@@ -41,8 +41,6 @@ SDA_DEV uint32_t canon_varint(uint64_t z, const ModParams& mp, bool& bad) {
   return r == 0 ? 0u : mp.m - r;
 }
 
-typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
-
 // Two candidate values from a word holding two (previous byte, byte) pairs in
 // its 16-bit halves: z = prev-is-continuation ? byte<<7 | prev&0x7f : byte,
 // then zigzag-decode and reduce a value in (-m, m) into [0, m). Halves whose

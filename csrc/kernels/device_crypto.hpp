@@ -19,6 +19,9 @@
 
 namespace sdagpu {
 
+// two u16 lanes of a 32-bit register (v_pk_*_u16)
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+
 SDA_DEV uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
 SDA_DEV uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
 

@@ -355,6 +355,185 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   }
 }
 
+// ------------------------------------- additive, 16-bit draws, packed pairs ----
+// The same exact-uniform 16-bit draws as k_share_additive16, with every
+// per-value step after the ChaCha core done on packed u16 pairs (m <= 32768, so
+// a pair's modular sum / difference never leaves 16 bits):
+//   add/sub mod m   v_pk_add/sub_u16 + v_pk_min_u16 (3 ops per 2 values)
+//   byte counts     zigzag length 1 + (v >= 64) (+ (v >= 8192)): one add + mask
+//                   + v_bcnt per pair
+//   rejection       a v_pk_max_u16 sweep over the block's 16 words; only a wave
+//                   holding a rejected half walks the replacement path
+// and 8 count tiles per lane so the lane's spare-draw block (one ChaCha block)
+// is amortised over 256 draws. The per-value path of k_share_additive16 spent
+// as many VALU instructions as its ChaCha cores (the round is VALU-bound).
+constexpr int kGP = 8;  // count tiles (groups of 16 elements) per lane
+
+SDA_DEV uint32_t pk_add_mod(uint32_t a, uint32_t b, u16x2 mm) {
+  const u16x2 t = __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b);
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(t, t - mm));
+}
+SDA_DEV uint32_t pk_sub_mod(uint32_t a, uint32_t b, u16x2 mm) {
+  const u16x2 t = __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b);
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(t, t + mm));
+}
+// x mod m for a 16-bit x (q = floor(x * mu32 / 2^32) is floor(x/m) or one less)
+SDA_DEV uint32_t mod16(uint32_t x, const ModParams& mp) {
+  const uint32_t q = __umulhi(x, mp.mu32);
+  const uint32_t r = x - __umul24(q, mp.m);
+  return min(r, r - mp.m);
+}
+// zigzag-varint bytes of the two canonical values of a pair (< 2^15)
+template <bool kShort>
+SDA_DEV uint32_t pk_vlen(uint32_t p) {
+  uint32_t n = 2u + __builtin_popcount((p + 0x7fc07fc0u) & 0x80008000u);  // v >= 64
+  if constexpr (!kShort) n += __builtin_popcount((p + 0x60006000u) & 0x80008000u);  // v >= 8192
+  return n;
+}
+
+// byte count of the first `valid` of 16 values held as 8 pairs
+template <bool kShort>
+SDA_DEV uint32_t pairs_bytes(const uint32_t (&vp)[8], int valid) {
+  uint32_t bytes = 0;
+  if (valid == 16) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) bytes += pk_vlen<kShort>(vp[k]);
+  } else {
+    for (int i = 0; i < valid; ++i) bytes += vlen((vp[i >> 1] >> (16 * (i & 1))) & 0xffffu);
+  }
+  return bytes;
+}
+SDA_DEV void store_pairs(uint16_t* dst, const uint32_t (&vp)[8], int valid, bool vec_ok) {
+  if (vec_ok && valid == 16) {
+    reinterpret_cast<uint4*>(dst)[0] = make_uint4(vp[0], vp[1], vp[2], vp[3]);
+    reinterpret_cast<uint4*>(dst)[1] = make_uint4(vp[4], vp[5], vp[6], vp[7]);
+  } else {
+    for (int i = 0; i < valid; ++i) dst[i] = (uint16_t)(vp[i >> 1] >> (16 * (i & 1)));
+  }
+}
+
+template <int MASK, bool kShort>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+    k_share_additive16p(int P, int D, int n, ModParams mp, uint32_t zone16,
+                        const int32_t* __restrict__ secrets, RngKeyArg rng, uint64_t owner_base,
+                        uint16_t* __restrict__ shares, uint32_t* __restrict__ cnt,
+                        uint32_t* __restrict__ mask_out, uint32_t* __restrict__ mask_cnt) {
+  __shared__ uint32_t partial[kMaxRows16 + 1][kGP][kWaves];
+  const int blk = blockIdx.x, p = blockIdx.y;
+  const int T = (D + kTileValues - 1) / kTileValues;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint64_t owner = owner_base + (uint64_t)p;
+  const RngKey rk = to_key(rng);
+  const uint32_t m = mp.m;
+  const u16x2 mm = {(uint16_t)m, (uint16_t)m};
+  const bool vec_ok = (D % 16) == 0;
+  constexpr int kMaskRows = MASK == kMaskFull ? 1 : 0;
+  const int rows = kMaskRows + (n - 1);
+  const int64_t Gtot = ((int64_t)D + 15) / 16;
+  const uint64_t lane_id = (uint64_t)blk * kBlock + tid;
+
+  uint32_t rw[16];  // this lane's spare halves
+  rng_block(rw, rk, stream_id(kPurposeRetry16, owner), lane_id);
+  uint32_t rused = 0;
+  uint16_t* lastrow = shares + ((size_t)(n - 1) * P + p) * D;
+
+#pragma unroll 1
+  for (int g = 0; g < kGP; ++g) {
+    const int e0 = blk * (kGP * kTileValues) + g * kTileValues + tid * 16;
+    const int valid = max(0, min(16, D - e0));
+    uint32_t lastp[8];  // the (masked) secret, becoming secret - sum(random shares)
+    {
+      uint32_t s[16];
+      load16_secrets(s, secrets + (size_t)p * D + e0, valid, vec_ok, mp);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) lastp[k] = s[2 * k] | (s[2 * k + 1] << 16);
+    }
+    for (int q = 0; 2 * q < rows; ++q) {
+      uint32_t w[16];
+      rng_block(w, rk, stream_id(kPurposeShares16, owner), (uint64_t)q * Gtot + e0 / 16);
+      // rejected halves (>= zone16, probability (2^16 mod m) / 2^16 each) are
+      // replaced by the lane's next accepted spare; the wave-uniform test keeps
+      // the walk out of waves that have none
+      u16x2 hmax = __builtin_bit_cast(u16x2, w[0]);
+#pragma unroll
+      for (int k = 1; k < 16; ++k) hmax = __builtin_elementwise_max(hmax, __builtin_bit_cast(u16x2, w[k]));
+      const bool any_rej = hmax.x >= zone16 || hmax.y >= zone16;
+      if (__builtin_amdgcn_ballot_w64(any_rej) != 0 && any_rej) {
+        uint32_t rej = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          rej |= (((w[k] & 0xffffu) >= zone16 ? 1u : 0u) | ((w[k] >> 16) >= zone16 ? 2u : 0u)) << (2 * k);
+        while (rej) {
+          const int b = __builtin_ctz(rej);
+          rej &= rej - 1;
+          uint32_t x = 0xffffffffu;
+          while (rused < 32 && x >= zone16) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) word = (k == (int)(rused >> 1)) ? rw[k] : word;
+            x = (word >> (16 * (rused & 1))) & 0xffffu;
+            ++rused;
+          }
+          if (x >= zone16) {  // spares exhausted: an exact draw from the per-element retry stream
+            const int row = 2 * q + (b >> 4);
+            x = uniform_fixup(rk, kPurposeSharesRetry, owner,
+                              ((uint64_t)row << 40) | (uint64_t)(e0 + ((b >> 1) & 7) * 2 + (b & 1)), m,
+                              (uint32_t)mp.zone32);
+          }
+          const uint32_t sh = 16u * (uint32_t)(b & 1);
+#pragma unroll
+          for (int k = 0; k < 16; ++k)
+            if (k == (b >> 1)) w[k] = (w[k] & ~(0xffffu << sh)) | (x << sh);
+        }
+      }
+      uint32_t bytes2 = 0;  // this pair of rows' byte counts in the two halves
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = 2 * q + h;
+        if (row >= rows) break;
+        const bool is_mask = row < kMaskRows;
+        uint32_t vp[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          vp[k] = mod16(w[8 * h + k] & 0xffffu, mp) | (mod16(w[8 * h + k] >> 16, mp) << 16);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          lastp[k] = is_mask ? pk_add_mod(lastp[k], vp[k], mm) : pk_sub_mod(lastp[k], vp[k], mm);
+        bytes2 |= pairs_bytes<kShort>(vp, valid) << (16 * h);
+        if (is_mask) {
+          uint32_t v[16];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { v[2 * k] = vp[k] & 0xffffu; v[2 * k + 1] = vp[k] >> 16; }
+          store16<uint32_t>(mask_out + (size_t)p * D + e0, v, valid, vec_ok);
+        } else {
+          store_pairs(shares + ((size_t)(row - kMaskRows) * P + p) * D + e0, vp, valid, vec_ok);
+        }
+      }
+      bytes2 = wave_sum(bytes2);  // both rows at once (each < 2^16)
+      if (lane == 0) {
+        partial[2 * q][g][wave] = bytes2 & 0xffffu;
+        if (2 * q + 1 < rows) partial[2 * q + 1][g][wave] = bytes2 >> 16;
+      }
+    }
+    store_pairs(lastrow + e0, lastp, valid, vec_ok);
+    const uint32_t bytes = wave_sum(pairs_bytes<kShort>(lastp, valid));
+    if (lane == 0) partial[kMaxRows16][g][wave] = bytes;
+  }
+  __syncthreads();
+  for (int x = tid; x < (rows + 1) * kGP; x += kBlock) {
+    const int r = x / kGP, g = x % kGP;
+    const int prow = r < rows ? r : kMaxRows16;
+    const int t = blk * kGP + g;
+    if (t >= T) continue;
+    uint32_t s = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += partial[prow][g][w];
+    if (r < kMaskRows) mask_cnt[(size_t)p * T + t] = s;
+    else if (r < rows) cnt[((size_t)(r - kMaskRows) * P + p) * T + t] = s;
+    else cnt[((size_t)(n - 1) * P + p) * T + t] = s;
+  }
+}
+
 // --------------------------------------------------------- packed Shamir ----
 constexpr int kPssMaxK = 8;
 constexpr int kPssMaxT = 16;
@@ -537,8 +716,22 @@ void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, con
     hipLaunchKernelGGL(k_chacha_seeds, dim3((P + 63) / 64), dim3(64), 0, s, P, seed_words, rng,
                        owner_base, seeds);
   // 16-bit draws: u16 shares, no ChaCha mask, room for the rows in LDS
-  if (g_share16 && value_bytes == 2 && m < 65536u && mask_mode != kMaskChaCha &&
-      (n - 1) + (mask_mode == kMaskFull ? 1 : 0) <= kMaxRows16) {
+  const bool rows_ok = (n - 1) + (mask_mode == kMaskFull ? 1 : 0) <= kMaxRows16;
+  if (g_share16 && value_bytes == 2 && m <= 32768u && mask_mode != kMaskChaCha && rows_ok) {
+    const uint32_t zone16 = 65536u - (65536u % m);
+    dim3 grid((D + kGP * kTileValues - 1) / (kGP * kTileValues), P);
+#define SDA_P16(MK, SH)                                                                      \
+  hipLaunchKernelGGL((k_share_additive16p<MK, SH>), grid, dim3(kBlock), 0, s, P, D, n, mp, zone16, \
+                     secrets, rng, owner_base, (uint16_t*)shares, cnt, mask_out, mask_cnt)
+    if (mask_mode == kMaskFull) {
+      if (m <= 8192u) SDA_P16(kMaskFull, true); else SDA_P16(kMaskFull, false);
+    } else {
+      if (m <= 8192u) SDA_P16(kMaskNone, true); else SDA_P16(kMaskNone, false);
+    }
+#undef SDA_P16
+    return;
+  }
+  if (g_share16 && value_bytes == 2 && m < 65536u && mask_mode != kMaskChaCha && rows_ok) {
     const uint32_t zone16 = 65536u - (65536u % m);
     dim3 grid16((D + kG16 * kTileValues - 1) / (kG16 * kTileValues), P);
     if (mask_mode == kMaskFull)

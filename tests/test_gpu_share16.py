@@ -38,7 +38,7 @@ def _run(m, n, P, D, mask):
     return sh
 
 
-@pytest.mark.parametrize("m", [433, 40000, 65521, 2])
+@pytest.mark.parametrize("m", [433, 40000, 65521, 2, 8192, 8193, 20000, 32768])
 @pytest.mark.parametrize("n,mask", [(3, False), (2, True), (5, True), (8, False)])
 def test_share16_exact(cuda, m, n, mask):
     _run(m, n, 3, 70001, mask)  # D not a multiple of the 16384-element block
