@@ -276,6 +276,88 @@ SDA_DEV P130 p130_pow(P130 r, uint32_t e) {
   }
   return acc;
 }
+// Fully reduced representative of h (limbs < 2^26, value < p).
+SDA_DEV P130 p130_freeze(const P130& x) {
+  uint32_t h0 = x.v[0], h1 = x.v[1], h2 = x.v[2], h3 = x.v[3], h4 = x.v[4], c;
+  c = h0 >> 26; h0 &= kM26; h1 += c;
+  c = h1 >> 26; h1 &= kM26; h2 += c;
+  c = h2 >> 26; h2 &= kM26; h3 += c;
+  c = h3 >> 26; h3 &= kM26; h4 += c;
+  c = h4 >> 26; h4 &= kM26; h0 += c * 5;
+  c = h0 >> 26; h0 &= kM26; h1 += c;
+  c = h1 >> 26; h1 &= kM26; h2 += c;
+  uint32_t g0 = h0 + 5; c = g0 >> 26; g0 &= kM26;
+  uint32_t g1 = h1 + c; c = g1 >> 26; g1 &= kM26;
+  uint32_t g2 = h2 + c; c = g2 >> 26; g2 &= kM26;
+  uint32_t g3 = h3 + c; c = g3 >> 26; g3 &= kM26;
+  uint32_t g4 = h4 + c - (1u << 26);
+  const uint32_t keep = (g4 >> 31) - 1;  // all ones iff h >= p
+  return P130{{(h0 & ~keep) | (g0 & keep), (h1 & ~keep) | (g1 & keep), (h2 & ~keep) | (g2 & keep),
+               (h3 & ~keep) | (g3 & keep), (h4 & ~keep) | (g4 & keep)}};
+}
+// 2^x mod p for x < 156 (2^130 = 5).
+SDA_DEV P130 p130_bit(int x) {
+  P130 r = p130_zero();
+  if (x < 130) r.v[x / 26] = 1u << (x % 26);
+  else r.v[0] = 5u << (x - 130);
+  return r;
+}
+// 7-bit digit d (bits 7d .. 7d+6) of a frozen value, d < 19.
+SDA_DEV uint32_t p130_digit7(const P130& w, int d) {
+  const int bit = 7 * d, li = bit / 26, sh = bit % 26;
+  uint64_t x = w.v[li];
+  if (li < 4) x |= (uint64_t)w.v[li + 1] << 26;
+  return (uint32_t)(x >> sh) & 0x7fu;
+}
+
+// ---- Poly1305 on the matrix cores (k_mac_chunks, tables from k_poly_powers) ----
+// A 1 KiB segment of 64 full blocks c_j (j = 0..63, bytes u_pos, pos = 16 j + a)
+// contributes h = sum_j c_j r^(64 - j) = sum_pos u_pos W(pos) + 2^128 sum_e r^e
+// with the key-dependent weights W(pos) = 2^(8a) r^(64 - j) mod p. Splitting W
+// into 19 digits D_d of 7 bits turns the sum into 19 integer dot products over
+// the segment's bytes -- an int8 GEMM: the i8 MFMA takes the bytes recentred
+// to u - 128 (signed) and the digits (0..127); per digit the dot product
+// C_d lies in (-2^24, 2^24). With x_d = C_d + 2^24 >= 0:
+//   h = sum_d x_d 2^(7d) + K_seg,
+//   K_seg = 2^128 sum_{e=1..64} r^e + 128 sum_pos W(pos) - 2^24 sum_d 2^(7d)  (mod p).
+SDA_DEV P130 poly_weight(const P130& rpow, int a) {
+  return p130_freeze(p130_mul(rpow, p130_bit(8 * a)));
+}
+// K_seg from sum_e r^e and sum_pos W(pos) (both carried, limbs < 2^27).
+SDA_DEV P130 poly_kseg(const P130& sum_r, const P130& sum_w) {
+  const P130 t1 = p130_mul(sum_r, p130_bit(128));
+  const P130 t2 = p130_mul(sum_w, P130{{128u, 0, 0, 0, 0}});
+  P130 b = p130_zero();
+#pragma unroll
+  for (int d = 0; d < 19; ++d) b = p130_add(b, p130_bit(24 + 7 * d));  // distinct bits: no carries
+  P130 k;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const uint32_t four_p = 4u * (i == 0 ? kM26 - 4u : kM26);
+    k.v[i] = t1.v[i] + t2.v[i] + four_p - b.v[i];
+  }
+  return p130_carry(k);
+}
+// Segment value from its 19 digit dot products C_d (summed over K-slices).
+SDA_DEV P130 poly_seg_value(const int32_t (&c)[19], const P130& kseg) {
+  uint32_t l[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int d = 0; d < 19; ++d) {
+    const uint32_t x = (uint32_t)(c[d] + (1 << 24));  // < 2^25
+    const int bit = 7 * d, li = bit / 26, sh = bit % 26;
+    const uint64_t v = (uint64_t)x << sh;
+    l[li] += (uint32_t)v & kM26;
+    l[li + 1] += (uint32_t)(v >> 26);
+  }
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    l[i + 1] += l[i] >> 26;
+    l[i] &= kM26;
+  }
+  const P130 h = p130_carry(P130{{l[0] + 5u * l[5], l[1], l[2], l[3], l[4]}});
+  return p130_carry(p130_add(h, kseg));
+}
+
 // Final tag = (h mod p + s) mod 2^128, as 4 LE words.
 SDA_DEV void p130_finish(uint32_t (&tag)[4], P130 h, const uint32_t (&s)[4]) {
   uint32_t h0 = h.v[0], h1 = h.v[1], h2 = h.v[2], h3 = h.v[3], h4 = h.v[4], c;

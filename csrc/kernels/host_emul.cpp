@@ -127,6 +127,98 @@ static void emul_mac(uint32_t (&tag)[4], const MsgKey& key, const uint8_t* ctbyt
   p130_finish(tag, H, s4);
 }
 
+// emulate k_poly_powers tables + the matrix-core k_mac_chunks<0> + k_mac_final
+// (the MFMA is an explicit integer dot product; the irregular-segment lanes run
+// the same Horner code as the device)
+static void emul_mac_mfma(uint32_t (&tag)[4], const MsgKey& key, const uint8_t* ctbytes, uint32_t N) {
+  const int C = kChunkBytes;
+  const int K = (int)(((int64_t)N + 32 + C - 1) / C);
+  const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
+  const P130 r = p130_r_from_key(rk);
+  // tables
+  std::vector<P130> fac(256);
+  P130 r4 = p130_mul(r, r);
+  r4 = p130_mul(r4, r4);
+  for (int t = 0; t < 256; ++t) fac[t] = p130_carry(p130_pow(r4, (uint32_t)(255 - t)));
+  std::vector<P130> rp(64);
+  for (int t = 0; t < 64; ++t) rp[t] = p130_carry(p130_pow(r, (uint32_t)(64 - t)));
+  std::vector<int8_t> tab(kPolyDigits * kSegBytes);
+  uint64_t sw[5] = {0, 0, 0, 0, 0}, sr[5] = {0, 0, 0, 0, 0};
+  for (int pos = 0; pos < kSegBytes; ++pos) {
+    const P130 w = poly_weight(rp[pos / 16], pos % 16);
+    for (int u = 0; u < 5; ++u) sw[u] += w.v[u];
+    for (int d = 0; d < kPolyDigits; ++d) tab[d * kSegBytes + pos] = (int8_t)p130_digit7(w, d);
+  }
+  for (int t = 0; t < 64; ++t)
+    for (int u = 0; u < 5; ++u) sr[u] += rp[t].v[u];
+  auto carry64 = [](uint64_t (&d)[5]) {
+    uint64_t c;
+    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+    c = d[1] >> 26; d[1] &= kM26; d[2] += c;
+    c = d[2] >> 26; d[2] &= kM26; d[3] += c;
+    c = d[3] >> 26; d[3] &= kM26; d[4] += c;
+    c = d[4] >> 26; d[4] &= kM26; d[0] += c * 5;
+    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+    return P130{{(uint32_t)d[0], (uint32_t)d[1], (uint32_t)d[2], (uint32_t)d[3], (uint32_t)d[4]}};
+  };
+  const P130 kseg = poly_kseg(carry64(sr), carry64(sw));
+  std::vector<P130> parts(K);
+  for (int k = 0; k < K; ++k) {
+    std::vector<uint8_t> buf(C, 0xAA);
+    const int64_t kC = (int64_t)k * C;
+    const int64_t start = kC >= 32 ? kC - 32 : 0;
+    const int64_t end = std::min((int64_t)N, kC + C - 32);
+    if (start >= end) { parts[k] = p130_zero(); continue; }
+    for (int64_t pos = start; pos < end; ++pos) buf[pos - (kC - 32)] = ctbytes[pos];
+    const int64_t fb = start / 16, eb = (end + 15) / 16, nfull = N / 16;
+    uint64_t d[5] = {0, 0, 0, 0, 0};
+    for (int s = 0; s < 16; ++s) {
+      const int64_t lo = eb - 64 * (int64_t)(16 - s);
+      if (lo >= fb && lo + 64 <= nfull) {  // regular: "MFMA" row
+        int32_t c[kPolyDigits];
+        for (int dd = 0; dd < kPolyDigits; ++dd) {
+          int32_t acc = 0;
+          for (int pos = 0; pos < kSegBytes; ++pos) {
+            const int8_t a = (int8_t)(buf[32 + 16 * lo - kC + pos] ^ 0x80);
+            acc += (int32_t)a * tab[dd * kSegBytes + pos];
+          }
+          c[dd] = acc;
+        }
+        const P130 h = p130_mul(poly_seg_value(c, kseg), fac[16 * s + 15]);
+        for (int u = 0; u < 5; ++u) d[u] += h.v[u];
+      } else if (lo + 64 > fb) {  // irregular: lanes 16 s .. 16 s + 15
+        for (int tid = 16 * s; tid < 16 * s + 16; ++tid) {
+          P130 hh = p130_zero();
+          for (int q = 0; q < 4; ++q) {
+            const int64_t i = eb - 4 * (int64_t)(256 - tid) + q;
+            P130 cb = p130_zero();
+            if (i >= fb) cb = load_block(buf.data(), i, kC, N);
+            hh = p130_mul(p130_add(hh, cb), r);
+          }
+          hh = p130_mul(hh, fac[tid]);
+          for (int u = 0; u < 5; ++u) d[u] += hh.v[u];
+        }
+      }
+    }
+    parts[k] = carry64(d);
+  }
+  const P130 rC = p130_pow(r, C / 16);
+  P130 H = p130_zero();
+  int64_t prev = 0;
+  for (int k = 0; k < K; ++k) {
+    const int64_t e = (k < K - 1) ? ((int64_t)(k + 1) * C - 32) / 16 : ((int64_t)N + 15) / 16;
+    if (k == 0) H = parts[k];
+    else {
+      const int64_t dd = e - prev;
+      const P130 Rd = (dd == C / 16) ? rC : p130_pow(r, (uint32_t)dd);
+      H = p130_carry(p130_add(p130_mul(H, Rd), parts[k]));
+    }
+    prev = e;
+  }
+  const uint32_t s4[4] = {key.poly_s[0], key.poly_s[1], key.poly_s[2], key.poly_s[3]};
+  p130_finish(tag, H, s4);
+}
+
 int main() {
   // 1. primitives vs host
   for (int it = 0; it < 20; ++it) {
@@ -203,6 +295,42 @@ int main() {
     uint8_t dtb[16];
     bytes(dtb, dt, 4);
     CHECK(std::memcmp(tag, dtb, 16) == 0, "poly1305 chunked N=%u", N);
+  }
+  // 4. matrix-core MAC formulation vs host poly1305 (segment-aligned, partial
+  //    last blocks, single-chunk, multi-chunk, all-0xff bytes)
+  for (uint32_t N : {0u, 1u, 15u, 16u, 17u, 100u, 1000u, 1024u, 1055u, 2047u, 16351u, 16352u,
+                     16353u, 16368u, 32704u, 40000u, 65536u, 100000u, 100001u}) {
+    for (int fill = 0; fill < 2; ++fill) {
+      std::vector<uint8_t> ct(N + 16);
+      if (fill) std::memset(ct.data(), 0xff, ct.size());
+      else hc::os_random(ct.data(), ct.size());
+      uint8_t tag[16];
+      hc::poly1305(tag, ct.data(), N, blk0);
+      uint32_t dt[4];
+      emul_mac_mfma(dt, mk, ct.data(), N);
+      uint8_t dtb[16];
+      bytes(dtb, dt, 4);
+      CHECK(std::memcmp(tag, dtb, 16) == 0, "poly1305 mfma N=%u fill=%d", N, fill);
+    }
+  }
+  // 5. random lengths up to 2 MB (MFMA formulation)
+  {
+    uint32_t seedw[1];
+    for (int it = 0; it < 300; ++it) {
+      hc::os_random(reinterpret_cast<uint8_t*>(seedw), 4);
+      uint32_t N = it < 150 ? seedw[0] % 2000000u : seedw[0] % 70000u;
+      if (it % 7 == 0) N &= ~15u;
+      if (it % 11 == 0) N = (N / kChunkBytes) * kChunkBytes + (uint32_t)(seedw[0] >> 24) * 4;
+      std::vector<uint8_t> ct(N + 16);
+      hc::os_random(ct.data(), ct.size());
+      uint8_t tag[16];
+      hc::poly1305(tag, ct.data(), N, blk0);
+      uint32_t dt[4];
+      emul_mac_mfma(dt, mk, ct.data(), N);
+      uint8_t dtb[16];
+      bytes(dtb, dt, 4);
+      CHECK(std::memcmp(tag, dtb, 16) == 0, "poly1305 mfma random N=%u", N);
+    }
   }
   std::printf(failures ? "host_emul: %d FAILURES\n" : "host_emul: all ok\n", failures);
   return failures ? 1 : 0;

@@ -35,6 +35,17 @@ constexpr int kSubBytes = 1024;     // terminator-count granularity (16 lanes x 
 constexpr int kSubPerChunk = kChunkBytes / kSubBytes;
 constexpr int kSumTile = 6144;      // elements per decode-sum tile (~11 KiB of varints at m = 433)
 
+// Per-message Poly1305 tables (k_poly_powers), kPowWords u32 per message:
+//   [0, 1280)         chunk factors r^(4(255-t)), t < 256, 5 x 26-bit limbs
+//   [1280, 1288)      segment constant K_seg (5 limbs; see seal.hip)
+//   [1288, kPowWords) int8 weight digits [kPolyDigits][kSegBytes]: 7-bit digit d of
+//                     W(pos) = 2^(8 (pos % 16)) r^(64 - pos / 16) mod p
+constexpr int kSegBytes = 1024;     // MFMA MAC row: one 64-block segment
+constexpr int kPolyDigits = 19;     // 7-bit digits of a value < 2^133
+constexpr int kPowKsegOff = 256 * 5;
+constexpr int kPowTabOff = kPowKsegOff + 8;
+constexpr int kPowWords = kPowTabOff + kPolyDigits * kSegBytes / 4;
+
 // Error bits (device error word)
 enum ErrBits : uint32_t {
   kErrBadKey = 1u,          // X25519 produced the all-zero point
@@ -109,13 +120,17 @@ void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
                            uint64_t stride, hipStream_t s);
 // Poly1305 chunk partials (and, when decrypt!=0, in-place decryption plus
 // varint-terminator counts per chunk).
-// Per-message Poly1305 chunk factors r^(4(255-t)), t = 0..255: pows [M][256][5].
+// Per-message Poly1305 tables pows [M][kPowWords]: chunk factors, segment
+// constant and weight digits of the matrix-core MAC (layout above).
 void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s);
 // With decrypt, term_cnt [M][K] (per chunk) and/or sub_cnt [M][K * kSubPerChunk]
 // (per 1 KiB sub-chunk) receive terminator counts (either may be null).
 void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,
                        uint64_t stride, const uint32_t* pt_len, uint32_t* partials, int decrypt,
                        uint32_t* term_cnt, uint32_t* sub_cnt, hipStream_t s);
+// Matrix-core Poly1305 segments (default on; 0 = per-lane Horner everywhere) --
+// benchmarking switch.
+void set_mac_mfma(int mode);
 // Combine partials -> tag; mode 0 = write the header mac, 1 = verify (ok[j]).
 void launch_mac_final(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,
                       const uint32_t* pt_len, const uint32_t* partials, int verify,

@@ -7,16 +7,21 @@
 //
 // Parallel Poly1305: a message is cut into 16 KiB chunks aligned to the keystream
 // (chunk k covers keystream bytes [kC, (k+1)C), i.e. message bytes
-// [kC-32, (k+1)C-32)). Inside a chunk each lane runs Horner over 4 consecutive
-// 16-byte blocks, end-aligned to the chunk's last block so that absent leading
-// blocks contribute exactly zero, and lanes are merged by a log-depth tree with
-// r^(4*2^l). A per-message pass chains the chunk partials with r^(C/16).
+// [kC-32, (k+1)C-32)). Inside a chunk the 16 segments of 64 blocks (aligned to
+// the chunk's last block) are the rows of an int8 GEMM against the message's
+// weight digits on the matrix cores (v_mfma_i32_16x16x64_i8; the algebra is in
+// device_crypto.hpp, poly_seg_value); segments holding a partial block or the
+// message start fall back to per-lane Horner over 4 blocks. Segment / lane sums
+// are placed by per-message factors r^(4(255-t)), and a per-message pass chains
+// the chunk partials with r^(C/16).
 #include "block_utils.hpp"
 #include "device_crypto.hpp"
 #include "kernels.hpp"
 
 namespace sdagpu {
 namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));  // one i8 MFMA operand fragment (16 bytes)
 
 constexpr int kValuesPerLane = kEncodeValues / kBlock;  // 32
 
@@ -160,11 +165,10 @@ __global__ void __launch_bounds__(kBlock) k_segscan(int T, uint32_t* __restrict_
   if (threadIdx.x == 0 && totals) totals[blockIdx.x] = carry;
 }
 
-// Read 16 plaintext/ciphertext bytes as a Poly1305 block (block index i of a
-// message of N bytes), from the chunk LDS image whose index 0 is keystream byte kC.
-SDA_DEV P130 load_block(const uint8_t* lds, int64_t i, int64_t kC, uint32_t N) {
-  const int64_t off = 32 + 16 * i - kC;
-  const uint4 q = *reinterpret_cast<const uint4*>(lds + off);
+// Read 16 ciphertext bytes as a Poly1305 block (block index i of a message of N
+// bytes at gmsg; a partial final block reads into the slot padding).
+SDA_DEV P130 load_block(const uint8_t* gmsg, int64_t i, uint32_t N) {
+  const uint4 q = *reinterpret_cast<const uint4*>(gmsg + 16 * i);
   uint32_t w[4] = {q.x, q.y, q.z, q.w};
   uint32_t hibit = 1u << 24;
   const int64_t rem = (int64_t)N - 16 * i;
@@ -186,81 +190,148 @@ SDA_DEV P130 load_block(const uint8_t* lds, int64_t i, int64_t kC, uint32_t N) {
 // 4-block Horner sum at its distance from the chunk end. Computed once per
 // message (it depends only on the key), so a chunk's combine is one multiply
 // per lane plus a sum -- instead of an 8-level multiply tree per chunk.
-__global__ void __launch_bounds__(kBlock)
-    k_poly_powers(const MsgKey* __restrict__ keys, uint32_t* __restrict__ pows) {
-  __builtin_amdgcn_s_setprio(3);  // side-stream key work (see k_seal_setup)
-  const int j = blockIdx.x, t = threadIdx.x;
-  const MsgKey key = keys[j];
-  const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
-  const P130 r = p130_r_from_key(rk);
-  P130 r4 = p130_mul(r, r);
-  r4 = p130_mul(r4, r4);
-  const P130 f = p130_carry(p130_pow(r4, (uint32_t)(kBlock - 1 - t)));
-  uint32_t* o = pows + ((size_t)j * kBlock + t) * 5;
-#pragma unroll
-  for (int u = 0; u < 5; ++u) o[u] = f.v[u];
-}
-
 SDA_DEV uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
 
-template <int DECRYPT>
+// Block sum of P130 values (limbs < 2^28) -> carried P130 on every thread.
+SDA_DEV P130 block_sum_p130(const P130& h, uint64_t (*red)[kWaves]) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();  // red reuse
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const uint64_t s = wave_sum64((uint64_t)h.v[u]);
+    if (lane == 0) red[u][wave] = s;
+  }
+  __syncthreads();
+  uint64_t d[5];
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    d[u] = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) d[u] += red[u][w];
+  }
+  uint64_t c;
+  c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+  c = d[1] >> 26; d[1] &= kM26; d[2] += c;
+  c = d[2] >> 26; d[2] &= kM26; d[3] += c;
+  c = d[3] >> 26; d[3] &= kM26; d[4] += c;
+  c = d[4] >> 26; d[4] &= kM26; d[0] += c * 5;
+  c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+  return P130{{(uint32_t)d[0], (uint32_t)d[1], (uint32_t)d[2], (uint32_t)d[3], (uint32_t)d[4]}};
+}
+
+// Per-message Poly1305 tables (layout: kernels.hpp kPow*):
+//  * r^(4 (255 - t)) for t = 0..255: the factor that places lane t's 4-block
+//    Horner sum (or segment t/16's value, at t = 16 s + 15) at its distance
+//    from the chunk end, so a chunk's combine is one multiply per term;
+//  * the 7-bit digits of the segment weights W(pos) and the segment constant
+//    K_seg of the matrix-core MAC (device_crypto.hpp, poly_seg_value).
+// Depends only on the key: computed once per message on the side stream.
 __global__ void __launch_bounds__(kBlock)
-    k_mac_chunks(const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
-                 uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
-                 uint32_t* __restrict__ partials, uint32_t* __restrict__ term_cnt,
-                 uint32_t* __restrict__ sub_cnt) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kChunkBytes];
+    k_poly_powers(const MsgKey* __restrict__ keys, uint32_t* __restrict__ pows) {
+  __builtin_amdgcn_s_setprio(3);  // side-stream key work (see k_seal_setup)
+  __shared__ P130 rp[64];
+  __shared__ uint64_t red[5][kWaves];
+  const int j = blockIdx.x, t = threadIdx.x;
+  const MsgKey key = keys[j];
+  const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
+  const P130 r = p130_r_from_key(rk);
+  uint32_t* base = pows + (size_t)j * kPowWords;
+  {
+    P130 r4 = p130_mul(r, r);
+    r4 = p130_mul(r4, r4);
+    const P130 f = p130_carry(p130_pow(r4, (uint32_t)(kBlock - 1 - t)));
+#pragma unroll
+    for (int u = 0; u < 5; ++u) base[t * 5 + u] = f.v[u];
+  }
+  // r^(64 - jb) for the segment's blocks jb = 0..63
+  P130 mine = p130_zero();
+  if (t < 64) {
+    mine = p130_carry(p130_pow(r, (uint32_t)(64 - t)));
+    rp[t] = mine;
+  }
+  __syncthreads();
+  // weights of positions 4t .. 4t+3 (block t/4, bytes 4(t%4) ..): one u32 of
+  // digits per (digit plane, thread)
+  const P130 rpow = rp[t >> 2];
+  uint32_t dig[kPolyDigits];
+#pragma unroll
+  for (int d = 0; d < kPolyDigits; ++d) dig[d] = 0;
+  P130 wsum = p130_zero();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const P130 w = poly_weight(rpow, 4 * (t & 3) + u);
+    wsum = p130_add(wsum, w);
+#pragma unroll
+    for (int d = 0; d < kPolyDigits; ++d) dig[d] |= p130_digit7(w, d) << (8 * u);
+  }
+  uint32_t* tab = base + kPowTabOff;
+#pragma unroll
+  for (int d = 0; d < kPolyDigits; ++d) tab[d * (kSegBytes / 4) + t] = dig[d];
+  const P130 sw = block_sum_p130(wsum, red);
+  const P130 sr = block_sum_p130(mine, red);
+  if (t == 0) {
+    const P130 k = poly_kseg(sr, sw);
+#pragma unroll
+    for (int u = 0; u < 5; ++u) base[kPowKsegOff + u] = k.v[u];
+  }
+}
+
+constexpr int kMacChunksPerBlock = 8;  // k_mac_chunks: chunks of one message per block
+
+// Index of a message's last chunk (chunk k covers message bytes [kC - 32, (k+1)C - 32)).
+SDA_DEV int last_chunk(uint32_t N) { return (int)(((int64_t)N + 31) / kChunkBytes); }
+
+// Per-lane Horner Poly1305 partial of chunk k: lane t sums the 4 blocks ending
+// 4 (255 - t) blocks before the chunk end eb (end-aligned, so blocks before the
+// message start contribute zero) and scales by its factor r^(4 (255 - t)).
+// Handles what the matrix-core rows do not: a message's first chunk (its first
+// 32 bytes precede the message) and its last chunk (partial final block, short
+// tail). With all != 0 it runs every chunk (A/B measurement of the MFMA path).
+__global__ void __launch_bounds__(kBlock)
+    k_mac_horner(int K, const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
+                 const uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
+                 uint32_t* __restrict__ partials, int all) {
   __shared__ uint64_t lsum[5][kWaves];
-  __shared__ uint32_t scratch[kWaves];
-  const int k = blockIdx.x, j = blockIdx.y, K = gridDim.x;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int j = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint32_t N = pt_len[j];
+  const int last = last_chunk(N);
+  int k;
+  if (all) {
+    k = blockIdx.x;
+    if (k > last) return;  // k_mac_chunks zeroes chunks past the message
+  } else {
+    k = blockIdx.x == 0 ? 0 : last;
+    if (blockIdx.x == 1 && last == 0) return;
+  }
   const int64_t kC = (int64_t)k * kChunkBytes;
   const int64_t start = kC >= 32 ? kC - 32 : 0;
   const int64_t end = min((int64_t)N, kC + kChunkBytes - 32);
   uint32_t* part = partials + ((size_t)j * K + k) * 8;
-  if (start >= end) {  // chunk beyond the message (or empty message)
+  if (start >= end) {
     if (tid < 5) part[tid] = 0;
-    if (DECRYPT && term_cnt && tid == 0) term_cnt[(size_t)j * K + k] = 0;
-    if (DECRYPT && sub_cnt && tid < kSubPerChunk)
-      sub_cnt[((size_t)j * K + k) * kSubPerChunk + tid] = 0;
     return;
   }
-  uint8_t* gmsg = ct + (size_t)j * stride + 48;
-  // this lane's chunk factor (independent of the data: issue the loads first)
-  const uint32_t* pf = pows + ((size_t)j * kBlock + tid) * 5;
+  const uint8_t* gmsg = ct + (size_t)j * stride + 48;
+  const uint32_t* pf = pows + (size_t)j * kPowWords + tid * 5;
   const P130 f = P130{{pf[0], pf[1], pf[2], pf[3], pf[4]}};
-  // load the chunk (16-byte pieces overlapping [start, end))
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int off = 64 * tid + 16 * q;
-    const int64_t pos = kC - 32 + off;
-    if (pos >= start - 15 && pos >= 0 && pos < end)
-      *reinterpret_cast<uint4*>(buf + off) = *reinterpret_cast<const uint4*>(gmsg + pos);
-  }
-  __syncthreads();
-
-  // ---- Poly1305 partial over blocks [fb, eb): lane t Horner-sums 4 blocks
-  // ending 4 * (255 - t) blocks before the chunk end, then scales by its factor
   const MsgKey key = keys[j];
   const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
   const P130 r = p130_r_from_key(rk);
-  const int64_t fb = start / 16;
-  const int64_t eb = (end + 15) / 16;
-  P130 h = p130_zero();
+  const int64_t fb = start / 16, eb = (end + 15) / 16;
+  P130 c[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int64_t i = eb - 4 * (int64_t)(kBlock - tid) + q;
-    P130 c = p130_zero();
-    if (i >= fb) c = load_block(buf, i, kC, N);
-    h = p130_mul(p130_add(h, c), r);
+    c[q] = i >= fb ? load_block(gmsg, i, N) : p130_zero();
   }
+  P130 h = p130_zero();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) h = p130_mul(p130_add(h, c[q]), r);
   h = p130_mul(h, f);
-  // block-wide sum of the limbs (64-bit: 256 x 2^27 fits easily), then carry
   uint64_t sv[5];
 #pragma unroll
   for (int u = 0; u < 5; ++u) sv[u] = wave_sum64((uint64_t)h.v[u]);
@@ -268,7 +339,7 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
     for (int u = 0; u < 5; ++u) lsum[u][wave] = sv[u];
   }
-  __syncthreads();  // also orders every lane's MAC reads of buf before the in-place decrypt
+  __syncthreads();
   if (tid == 0) {
     uint64_t d[5];
 #pragma unroll
@@ -277,68 +348,192 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
       for (int w = 0; w < kWaves; ++w) d[u] += lsum[u][w];
     }
-    uint64_t c;
-    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
-    c = d[1] >> 26; d[1] &= kM26; d[2] += c;
-    c = d[2] >> 26; d[2] &= kM26; d[3] += c;
-    c = d[3] >> 26; d[3] &= kM26; d[4] += c;
-    c = d[4] >> 26; d[4] &= kM26; d[0] += c * 5;
-    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+    uint64_t cc;
+    cc = d[0] >> 26; d[0] &= kM26; d[1] += cc;
+    cc = d[1] >> 26; d[1] &= kM26; d[2] += cc;
+    cc = d[2] >> 26; d[2] &= kM26; d[3] += cc;
+    cc = d[3] >> 26; d[3] &= kM26; d[4] += cc;
+    cc = d[4] >> 26; d[4] &= kM26; d[0] += cc * 5;
+    cc = d[0] >> 26; d[0] &= kM26; d[1] += cc;
 #pragma unroll
     for (int u = 0; u < 5; ++u) part[u] = (uint32_t)d[u];
   }
+}
 
-  if constexpr (DECRYPT) {
-    // keystream block b covers message bytes [64b-32, 64b+32)
-    const int64_t b = kC / 64 + tid;
-    const int64_t lo = 64 * b - 32;
-    if (lo < end && lo + 64 > start) {
-      uint32_t w[16];
-      salsa20_block(w, key.subkey, key.nonce[0], key.nonce[1], (uint64_t)b);
-      uint4* q = reinterpret_cast<uint4*>(buf + 64 * tid);
+// Middle chunks on the matrix cores (+ in-place decryption and terminator
+// counts for every chunk when DECRYPT). A middle chunk (not the message's
+// first or last) is 16 full segments of 64 blocks, segment s = blocks
+// [fb + 64 s, fb + 64 (s + 1)), fb = kC/16 - 2: the 16 rows of an int8 GEMM
+// (device_crypto.hpp, poly_seg_value) with K = the segment's 1 KiB of bytes
+// (wave w takes bytes [256 w, 256 w + 256) of every row) and N = the 19 weight
+// digits (two 16-column tiles). Row s is then placed by r^(64 (15 - s)) =
+// factor t = 16 s + 15. First / last chunks are k_mac_horner's (launched
+// first: it reads the ciphertext this kernel decrypts in place).
+template <int DECRYPT>
+__global__ void __launch_bounds__(kBlock)
+    k_mac_chunks(int K, const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
+                 uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
+                 uint32_t* __restrict__ partials, uint32_t* __restrict__ term_cnt,
+                 uint32_t* __restrict__ sub_cnt, int use_mfma) {
+  __shared__ int32_t cpart[2][kWaves][16][kPolyDigits + 1];  // double-buffered per chunk
+  __shared__ uint32_t scratch[kWaves];
+  const int j = blockIdx.y;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int row = lane & 15, g = lane >> 4;
+  const uint32_t N = pt_len[j];
+  const int last = last_chunk(N);
+  uint8_t* gmsg = ct + (size_t)j * stride + 48;
+  const uint32_t* pw = pows + (size_t)j * kPowWords;
+  const int k0 = blockIdx.x * kMacChunksPerBlock;
+  const int k1 = min(K, k0 + kMacChunksPerBlock);
+  const bool any_middle = use_mfma && k1 > 1 && k0 < last && max(k0, 1) < min(k1, last);
+  // the message's weight-digit fragments (this lane's K-slice of its digit
+  // columns), segment constant and segment factors: loaded once, reused by
+  // every chunk of the block
+  v4i b0[4], b1[4];
+  P130 kseg = p130_zero(), sfac = p130_zero();
+  if (any_middle) {
+    const int8_t* tab = reinterpret_cast<const int8_t*>(pw + kPowTabOff);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        uint4 d = q[u];
-        d.x ^= w[4 * u]; d.y ^= w[4 * u + 1]; d.z ^= w[4 * u + 2]; d.w ^= w[4 * u + 3];
-        q[u] = d;
+    for (int qq = 0; qq < 4; ++qq) {
+      const int q = 4 * wave + qq;
+      b0[qq] = *reinterpret_cast<const v4i*>(tab + row * kSegBytes + 64 * q + 16 * g);
+      b1[qq] = v4i{0, 0, 0, 0};
+      if (row < kPolyDigits - 16)
+        b1[qq] = *reinterpret_cast<const v4i*>(tab + (16 + row) * kSegBytes + 64 * q + 16 * g);
+    }
+    if (wave == 0 && lane < 16) {
+      const uint32_t* pf = pw + (16 * lane + 15) * 5;
+#pragma unroll
+      for (int u = 0; u < 5; ++u) {
+        kseg.v[u] = pw[kPowKsegOff + u];
+        sfac.v[u] = pf[u];
       }
     }
-    // terminators (MSB clear) among this lane's valid bytes: 64-bit mask + popcount
-    const int64_t p0 = kC - 32 + 64 * tid;
-    const int vlo = (int)max((int64_t)0, start - p0);
-    const int vhi = (int)min((int64_t)64, end - p0);
-    uint64_t vmask = 0;
-    if (vhi > vlo) vmask = (vhi >= 64 ? ~0ull : ((1ull << vhi) - 1)) & ~((1ull << vlo) - 1);
-    uint64_t tmask = 0;
+  }
+  int buf = 0;
+  for (int k = k0; k < k1; ++k) {
+    const int64_t kC = (int64_t)k * kChunkBytes;
+    const int64_t start = kC >= 32 ? kC - 32 : 0;
+    const int64_t end = min((int64_t)N, kC + kChunkBytes - 32);
+    uint32_t* part = partials + ((size_t)j * K + k) * 8;
+    if (start >= end) {  // chunk beyond the message (or empty message)
+      if (tid < 5) part[tid] = 0;
+      if (DECRYPT && term_cnt && tid == 0) term_cnt[(size_t)j * K + k] = 0;
+      if (DECRYPT && sub_cnt && tid < kSubPerChunk)
+        sub_cnt[((size_t)j * K + k) * kSubPerChunk + tid] = 0;
+      continue;
+    }
+    // Decrypt side: this lane's 64 bytes = keystream block kC/64 + tid, i.e.
+    // message bytes [kC - 32 + 64 tid, +64) (16-byte pieces overlapping
+    // [start, end); the MAC loads below hit the same lines in cache).
+    uint4 pt4[4];
+    if constexpr (DECRYPT) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint4 d = *reinterpret_cast<const uint4*>(buf + 64 * tid + 16 * q);
-      const uint32_t ws[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t t = ~ws[u] & 0x80808080u;
-        const uint64_t bits = ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
-        tmask |= bits << (16 * q + 4 * u);
+      for (int q = 0; q < 4; ++q) {
+        const int64_t pos = kC - 32 + 64 * tid + 16 * q;
+        pt4[q] = make_uint4(0, 0, 0, 0);
+        if (pos >= start - 15 && pos >= 0 && pos < end) pt4[q] = *reinterpret_cast<const uint4*>(gmsg + pos);
       }
     }
-    const uint32_t cnt = (uint32_t)__popcll(tmask & vmask);
-    if (sub_cnt) {  // per 1 KiB sub-chunk: the 16 lanes covering it
-      uint32_t sc = cnt;
+    if (use_mfma && k != 0 && k != last) {
+      const int64_t lo = kC / 16 - 2 + 64 * row;  // first block of segment `row`
+      v4i a[4];
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) sc += __shfl_xor(sc, o, 64);
-      if ((tid & 15) == 0) sub_cnt[((size_t)j * K + k) * kSubPerChunk + (tid >> 4)] = sc;
-    }
-    if (term_cnt) {
-      const uint32_t tot = block_sum(cnt, scratch);
-      if (tid == 0) term_cnt[(size_t)j * K + k] = tot;
-    }
-    // store plaintext in place (bytes past `end` land in the slot padding)
+      for (int qq = 0; qq < 4; ++qq)
+        a[qq] = *reinterpret_cast<const v4i*>(gmsg + 16 * (lo + 4 * (4 * wave + qq) + g));
+      v4i acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int off = 64 * tid + 16 * q;
-      const int64_t pos = kC - 32 + off;
-      if (pos >= start - 15 && pos >= 0 && pos < end)
-        *reinterpret_cast<uint4*>(gmsg + pos) = *reinterpret_cast<const uint4*>(buf + off);
+      for (int qq = 0; qq < 4; ++qq) {
+        const v4i x = a[qq] ^ (int)0x80808080;  // bytes u -> u - 128 (signed)
+        acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, b0[qq], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, b1[qq], acc1, 0, 0, 0);
+      }
+      // C[segment 4 g + i][digit row]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        cpart[buf][wave][4 * g + i][row] = acc0[i];
+        if (row < kPolyDigits - 16) cpart[buf][wave][4 * g + i][16 + row] = acc1[i];
+      }
+      // all waves' partials are in (and every MAC read of the chunk is done
+      // before its in-place decryption); wave 0 reads this buffer while the
+      // others move on to the next chunk's, and passes the next barrier only
+      // after it is done
+      __syncthreads();
+      if (wave == 0) {
+        P130 h = p130_zero();
+        if (lane < 16) {
+          int32_t c[kPolyDigits];
+#pragma unroll
+          for (int d = 0; d < kPolyDigits; ++d)
+            c[d] = cpart[buf][0][lane][d] + cpart[buf][1][lane][d] + cpart[buf][2][lane][d] +
+                   cpart[buf][3][lane][d];
+          h = p130_mul(poly_seg_value(c, kseg), sfac);
+        }
+        uint64_t d[5];
+#pragma unroll
+        for (int u = 0; u < 5; ++u) d[u] = wave_sum64((uint64_t)h.v[u]);
+        if (lane == 0) {
+          uint64_t cc;
+          cc = d[0] >> 26; d[0] &= kM26; d[1] += cc;
+          cc = d[1] >> 26; d[1] &= kM26; d[2] += cc;
+          cc = d[2] >> 26; d[2] &= kM26; d[3] += cc;
+          cc = d[3] >> 26; d[3] &= kM26; d[4] += cc;
+          cc = d[4] >> 26; d[4] &= kM26; d[0] += cc * 5;
+          cc = d[0] >> 26; d[0] &= kM26; d[1] += cc;
+#pragma unroll
+          for (int u = 0; u < 5; ++u) part[u] = (uint32_t)d[u];
+        }
+      }
+      buf ^= 1;
+    }
+
+    if constexpr (DECRYPT) {
+      const MsgKey key = keys[j];
+      // keystream block b covers message bytes [64b-32, 64b+32)
+      const int64_t b = kC / 64 + tid;
+      const int64_t p0 = 64 * b - 32;
+      if (p0 < end && p0 + 64 > start) {
+        uint32_t w[16];
+        salsa20_block(w, key.subkey, key.nonce[0], key.nonce[1], (uint64_t)b);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          pt4[u].x ^= w[4 * u]; pt4[u].y ^= w[4 * u + 1]; pt4[u].z ^= w[4 * u + 2]; pt4[u].w ^= w[4 * u + 3];
+        }
+      }
+      // terminators (MSB clear) among this lane's valid bytes: 64-bit mask + popcount
+      const int vlo = (int)max((int64_t)0, start - p0);
+      const int vhi = (int)min((int64_t)64, end - p0);
+      uint64_t vmask = 0;
+      if (vhi > vlo) vmask = (vhi >= 64 ? ~0ull : ((1ull << vhi) - 1)) & ~((1ull << vlo) - 1);
+      uint64_t tmask = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t ws[4] = {pt4[q].x, pt4[q].y, pt4[q].z, pt4[q].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t t = ~ws[u] & 0x80808080u;
+          const uint64_t bits = ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+          tmask |= bits << (16 * q + 4 * u);
+        }
+      }
+      const uint32_t cnt = (uint32_t)__popcll(tmask & vmask);
+      if (sub_cnt) {  // per 1 KiB sub-chunk: the 16 lanes covering it
+        uint32_t sc = cnt;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) sc += __shfl_xor(sc, o, 64);
+        if ((tid & 15) == 0) sub_cnt[((size_t)j * K + k) * kSubPerChunk + (tid >> 4)] = sc;
+      }
+      if (term_cnt) {
+        const uint32_t tot = block_sum(cnt, scratch);
+        if (tid == 0) term_cnt[(size_t)j * K + k] = tot;
+      }
+      // store plaintext in place (bytes past `end` land in the slot padding)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t pos = p0 + 16 * q;
+        if (pos >= start - 15 && pos >= 0 && pos < end) *reinterpret_cast<uint4*>(gmsg + pos) = pt4[q];
+      }
     }
   }
 }
@@ -412,17 +607,24 @@ void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s
   hipLaunchKernelGGL(k_poly_powers, dim3(M), dim3(kBlock), 0, s, keys, pows);
 }
 
+static int g_mac_mfma = 1;
+void set_mac_mfma(int mode) { g_mac_mfma = mode; }
+
 void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,
                        uint64_t stride, const uint32_t* pt_len, uint32_t* partials, int decrypt,
                        uint32_t* term_cnt, uint32_t* sub_cnt, hipStream_t s) {
   if (M <= 0 || K <= 0) return;
-  dim3 grid(K, M);
+  // first / last chunks (every chunk when the matrix-core path is off) by
+  // Horner, ahead of the in-place decryption
+  hipLaunchKernelGGL(k_mac_horner, dim3(g_mac_mfma ? 2 : K, M), dim3(kBlock), 0, s, K, keys, pows,
+                     ct, stride, pt_len, partials, g_mac_mfma ? 0 : 1);
+  const dim3 grid_c((K + kMacChunksPerBlock - 1) / kMacChunksPerBlock, M);
   if (decrypt)
-    hipLaunchKernelGGL(k_mac_chunks<1>, grid, dim3(kBlock), 0, s, keys, pows, ct, stride, pt_len,
-                       partials, term_cnt, sub_cnt);
+    hipLaunchKernelGGL(k_mac_chunks<1>, grid_c, dim3(kBlock), 0, s, K, keys, pows, ct, stride,
+                       pt_len, partials, term_cnt, sub_cnt, g_mac_mfma);
   else
-    hipLaunchKernelGGL(k_mac_chunks<0>, grid, dim3(kBlock), 0, s, keys, pows, ct, stride, pt_len,
-                       partials, term_cnt, sub_cnt);
+    hipLaunchKernelGGL(k_mac_chunks<0>, grid_c, dim3(kBlock), 0, s, K, keys, pows, ct, stride,
+                       pt_len, partials, term_cnt, sub_cnt, g_mac_mfma);
 }
 
 void launch_mac_final(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,

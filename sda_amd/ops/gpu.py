@@ -16,7 +16,7 @@ SUB_BYTES = 1024                  # terminator-count granularity of the fused cl
 SUB_PER_CHUNK = CHUNK_BYTES // SUB_BYTES
 SUM_TILE = 6144                   # elements per decode-sum tile (k_decode_sum)
 MSGKEY_BYTES = 80
-POW_WORDS = 256 * 5  # Poly1305 chunk factors per message (k_poly_powers)
+POW_WORDS = 6152  # Poly1305 tables per message (k_poly_powers; kernels.hpp kPowWords)
 SEAL_OVERHEAD = 48
 
 MASK_NONE, MASK_FULL, MASK_CHACHA = 0, 1, 2
