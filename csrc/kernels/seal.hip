@@ -370,7 +370,7 @@ __global__ void __launch_bounds__(kBlock)
 // factor t = 16 s + 15. First / last chunks are k_mac_horner's (launched
 // first: it reads the ciphertext this kernel decrypts in place).
 template <int DECRYPT>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
     k_mac_chunks(int K, const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
                  uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
                  uint32_t* __restrict__ partials, uint32_t* __restrict__ term_cnt,
