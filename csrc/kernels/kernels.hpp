@@ -69,6 +69,9 @@ void launch_seal_setup(int M, RngKeyArg rng, uint64_t msg_owner_base, const uint
 void launch_open_setup(int M, const uint32_t* key_idx, const uint32_t* sks, const uint32_t* pks,
                        const uint8_t* ct, uint64_t stride, MsgKey* keys, uint32_t* err,
                        uint32_t* gate, uint32_t gate_val, hipStream_t s);
+// Wave priority of the open-side setup and the Poly1305 table kernels (1 = top;
+// default 0 = normal: neither is latency-critical) -- scheduling experiments.
+void set_key_prio(int open_prio, int powers_prio);
 // Dispatch gate: the setup kernels store gate_val to *gate (if non-null) when
 // their first workgroup starts; k_gate_wait (one wave) polls for it, giving up
 // after timeout_us. Orders a side-stream setup's dispatch before a main-stream

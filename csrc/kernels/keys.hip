@@ -118,9 +118,9 @@ __global__ void __launch_bounds__(64) k_open_setup(int M, const uint32_t* __rest
                                                    const uint32_t* __restrict__ pks,
                                                    const uint8_t* ct, uint64_t stride,
                                                    MsgKey* keys, uint32_t* err,
-                                                   uint32_t* gate, uint32_t gate_val) {
+                                                   uint32_t* gate, uint32_t gate_val, int prio) {
   signal_dispatched(gate, gate_val);
-  __builtin_amdgcn_s_setprio(3);  // see k_seal_setup
+  if (prio) __builtin_amdgcn_s_setprio(3);  // see k_seal_setup
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= M) return;
   const uint32_t* hdr = reinterpret_cast<const uint32_t*>(ct + (size_t)j * stride);
@@ -157,6 +157,13 @@ __global__ void __launch_bounds__(64) k_x25519(int N, const uint32_t* __restrict
 
 }  // namespace
 
+static int g_open_prio = 0;
+int g_powers_prio = 0;
+void set_key_prio(int open_prio, int powers_prio) {
+  g_open_prio = open_prio;
+  g_powers_prio = powers_prio;
+}
+
 void launch_seal_setup(int M, RngKeyArg rng, uint64_t owner_base, const uint32_t* key_idx,
                        const uint32_t* pks, uint8_t* ct, uint64_t stride, MsgKey* keys,
                        uint32_t* err, uint32_t* gate, uint32_t gate_val, hipStream_t s) {
@@ -171,7 +178,7 @@ void launch_open_setup(int M, const uint32_t* key_idx, const uint32_t* sks, cons
                        uint32_t* gate, uint32_t gate_val, hipStream_t s) {
   if (M <= 0) return;
   hipLaunchKernelGGL(k_open_setup, dim3((M + 63) / 64), dim3(64), 0, s, M, key_idx, sks, pks, ct,
-                     stride, keys, err, gate, gate_val);
+                     stride, keys, err, gate, gate_val, g_open_prio);
 }
 
 void launch_gate_wait(const uint32_t* gate, uint32_t val, uint32_t timeout_us, hipStream_t s) {

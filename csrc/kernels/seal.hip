@@ -231,8 +231,8 @@ SDA_DEV P130 block_sum_p130(const P130& h, uint64_t (*red)[kWaves]) {
 //    K_seg of the matrix-core MAC (device_crypto.hpp, poly_seg_value).
 // Depends only on the key: computed once per message on the side stream.
 __global__ void __launch_bounds__(kBlock)
-    k_poly_powers(const MsgKey* __restrict__ keys, uint32_t* __restrict__ pows) {
-  __builtin_amdgcn_s_setprio(3);  // side-stream key work (see k_seal_setup)
+    k_poly_powers(const MsgKey* __restrict__ keys, uint32_t* __restrict__ pows, int prio) {
+  if (prio) __builtin_amdgcn_s_setprio(3);  // side-stream key work (see k_seal_setup)
   __shared__ P130 rp[64];
   __shared__ uint64_t red[5][kWaves];
   const int j = blockIdx.x, t = threadIdx.x;
@@ -602,9 +602,11 @@ void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
                        (const uint32_t*)vals, tile_off, keys, ct, stride);
 }
 
+extern int g_powers_prio;  // keys.hip (set_key_prio)
+
 void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s) {
   if (M <= 0) return;
-  hipLaunchKernelGGL(k_poly_powers, dim3(M), dim3(kBlock), 0, s, keys, pows);
+  hipLaunchKernelGGL(k_poly_powers, dim3(M), dim3(kBlock), 0, s, keys, pows, g_powers_prio);
 }
 
 static int g_mac_mfma = 1;

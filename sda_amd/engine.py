@@ -33,6 +33,11 @@ from .ops.sealed import (Arena, open_, open_data, open_setup, open_sum, seal, se
 from .utils.trace import tracing_enabled
 
 _TRACE = tracing_enabled()
+# Experimental schedule switch: queue the clerks' key agreement behind the share
+# kernel instead of beside it (A/B measurement of side-stream interference).
+_OPEN_AFTER_SHARE = os.environ.get("SDA_OPEN_AFTER_SHARE", "1") == "1"
+# "open,powers" wave priorities of the side-stream key kernels (experiments)
+_KEY_PRIO = os.environ.get("SDA_KEY_PRIO")
 
 
 class AggregationError(RuntimeError):
@@ -83,6 +88,9 @@ class DeviceAggregator:
         self.vdtype = G.value_dtype(self.m)
         self.time_stages = time_stages
         self._round = 0
+        if _KEY_PRIO:
+            from ._native import gpu
+            gpu().set_key_prio(*[int(x) for x in _KEY_PRIO.split(",")])
         if isinstance(spec.sharing, PackedShamir):
             p = spec.sharing.native()
             p.validate()
@@ -430,19 +438,29 @@ class DeviceAggregator:
                        if mask_arena is not None else None)
             ev_sealkeys = torch.cuda.Event()
             ev_sealkeys.record(side)
-            ko_clerk = self._open_keys(clerk_arena, kidx_clerk, live, P, err) \
-                if local_clerks else None
-            ko_mask = (open_setup(mask_arena, kidx_rcpt_p, self.keys.sks, pks, err)
-                       if mask_arena is not None else None)
-            ev_openkeys = torch.cuda.Event()
-            ev_openkeys.record(side)
-        for t in [ks_clerk, ks_mask, ko_mask] + (ko_clerk or []):
-            if t is not None:
-                t.record_stream(main)
+
+        def open_keys():
+            with torch.cuda.stream(side):
+                ko_clerk = self._open_keys(clerk_arena, kidx_clerk, live, P, err) \
+                    if local_clerks else None
+                ko_mask = (open_setup(mask_arena, kidx_rcpt_p, self.keys.sks, pks, err)
+                           if mask_arena is not None else None)
+                ev_openkeys = torch.cuda.Event()
+                ev_openkeys.record(side)
+            return ko_clerk, ko_mask, ev_openkeys
+
+        if not _OPEN_AFTER_SHARE:
+            ko_clerk, ko_mask, ev_openkeys = open_keys()
 
         # ---- participants: mask + share, then encrypt (waits for the seal keys)
         G.gate_wait(gate)  # the setup waves are resident before the share grid
         shares, cnt, mask_vals, mask_cnt = self._share(secrets, rng_key, owner_base, err)
+        if _OPEN_AFTER_SHARE:
+            side.wait_stream(main)
+            ko_clerk, ko_mask, ev_openkeys = open_keys()
+        for t in [ks_clerk, ks_mask, ko_mask] + (ko_clerk or []):
+            if t is not None:
+                t.record_stream(main)
         main.wait_event(ev_sealkeys)
         seal_data(clerk_arena, ks_clerk, shares.view(n * P, B), err, cnt)
         del shares
