@@ -76,3 +76,25 @@ def test_distributed_device_ranks_one_gpu(cuda, world, name, layout):
     errs = [r[1] for r in results if r[0] == "err"]
     assert not errs, errs
     assert all(r[1] for r in results), results
+
+
+@pytest.mark.parametrize("layout", ["committee", "owner"])
+def test_bench_over_rccl_single_rank(cuda, layout):
+    """bench.py's distributed path on the real backend: torchrun, one rank,
+    `nccl` (RCCL) process group, the pipelined committee exchange (every
+    transfer is rank-local at world size 1) and the RCCL reduce / all-reduce /
+    barrier calls. bench.py checks the aggregate against the reference sum in
+    its first warmup round and exits non-zero on a mismatch."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "bench.py"), "--gpus", "1", "--force-dist", "--layout", layout,
+           "--steps", "2", "--warmup", "1", "--participants", "48", "--dim", "100000"]
+    out = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0
