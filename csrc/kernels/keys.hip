@@ -59,12 +59,17 @@ SDA_DEV void derive_msg_key(MsgKey& out, const uint32_t (&shared)[8], const uint
   out.pad[0] = out.pad[1] = 0;
 }
 
+// Setup kernels run beside full-chip grids: 4 ladder waves per workgroup pack
+// them onto a quarter as many CUs (a ~150-VGPR ladder wave costs its CU one of
+// the neighbouring grid's workgroups; measured on the round timeline).
+constexpr int kSetupBlock = 256;
+
 // Two lanes per message: the even lane computes epk = esk . 9, the odd lane the
 // shared point esk . pk -- the two ladders are independent, so running them side
 // by side halves the setup latency (one ladder per lane is ~1.7 ms whatever the
 // message count, and a round's first encode waits on these keys). The results
 // meet through a lane shuffle; the even lane derives the message key.
-__global__ void __launch_bounds__(64) k_seal_setup(int M, RngKeyArg rng, uint64_t owner_base,
+__global__ void __launch_bounds__(kSetupBlock) k_seal_setup(int M, RngKeyArg rng, uint64_t owner_base,
                                                    const uint32_t* __restrict__ key_idx,
                                                    const uint32_t* __restrict__ pks, uint8_t* ct,
                                                    uint64_t stride, MsgKey* keys, uint32_t* err,
@@ -113,7 +118,7 @@ __global__ void __launch_bounds__(64) k_seal_setup(int M, RngKeyArg rng, uint64_
   for (int i = 0; i < 8; ++i) hdr[i] = epk[i];
 }
 
-__global__ void __launch_bounds__(64) k_open_setup(int M, const uint32_t* __restrict__ key_idx,
+__global__ void __launch_bounds__(kSetupBlock) k_open_setup(int M, const uint32_t* __restrict__ key_idx,
                                                    const uint32_t* __restrict__ sks,
                                                    const uint32_t* __restrict__ pks,
                                                    const uint8_t* ct, uint64_t stride,
@@ -169,7 +174,8 @@ void launch_seal_setup(int M, RngKeyArg rng, uint64_t owner_base, const uint32_t
                        uint32_t* err, uint32_t* gate, uint32_t gate_val, hipStream_t s) {
   if (M <= 0) return;
   const int64_t threads = 2 * (int64_t)M;
-  hipLaunchKernelGGL(k_seal_setup, dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, s, M, rng,
+  hipLaunchKernelGGL(k_seal_setup, dim3((unsigned)((threads + kSetupBlock - 1) / kSetupBlock)),
+                     dim3(kSetupBlock), 0, s, M, rng,
                      owner_base, key_idx, pks, ct, stride, keys, err, gate, gate_val);
 }
 
@@ -177,7 +183,8 @@ void launch_open_setup(int M, const uint32_t* key_idx, const uint32_t* sks, cons
                        const uint8_t* ct, uint64_t stride, MsgKey* keys, uint32_t* err,
                        uint32_t* gate, uint32_t gate_val, hipStream_t s) {
   if (M <= 0) return;
-  hipLaunchKernelGGL(k_open_setup, dim3((M + 63) / 64), dim3(64), 0, s, M, key_idx, sks, pks, ct,
+  hipLaunchKernelGGL(k_open_setup, dim3((M + kSetupBlock - 1) / kSetupBlock), dim3(kSetupBlock), 0, s,
+                     M, key_idx, sks, pks, ct,
                      stride, keys, err, gate, gate_val, g_open_prio);
 }
 

@@ -317,10 +317,10 @@ class DeviceAggregator:
         gate = self._gate_token()
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            ks = seal_setup(arena, kidx, pks, rng_key, 0, err, gate=gate)
+            ks = seal_setup(arena, kidx, pks, rng_key, 0, err, gate=gate).with_powers()
             ks_mask = ko_mask = None
             if mask_arena is not None:
-                ks_mask = seal_setup(mask_arena, kidx_rcpt, pks, rng_key, n * P, err)
+                ks_mask = seal_setup(mask_arena, kidx_rcpt, pks, rng_key, n * P, err).with_powers()
                 ko_mask = open_setup(mask_arena, kidx_rcpt, sks, pks, err)
             ev_seal = torch.cuda.Event()
             ev_seal.record(side)
@@ -433,8 +433,10 @@ class DeviceAggregator:
         gate = self._gate_token()
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            ks_clerk = seal_setup(clerk_arena, kidx_clerk, pks, rng_key, 0, err, gate=gate)
-            ks_mask = (seal_setup(mask_arena, kidx_rcpt_p, pks, rng_key, n * P, err)
+            # Poly1305 tables on the side stream too: the encrypt is ~3 ms away
+            ks_clerk = seal_setup(clerk_arena, kidx_clerk, pks, rng_key, 0, err,
+                                  gate=gate).with_powers()
+            ks_mask = (seal_setup(mask_arena, kidx_rcpt_p, pks, rng_key, n * P, err).with_powers()
                        if mask_arena is not None else None)
             ev_sealkeys = torch.cuda.Event()
             ev_sealkeys.record(side)
@@ -555,7 +557,7 @@ class DeviceAggregator:
         with torch.cuda.stream(side):
             res_arena = Arena.empty(len(live), self.spec.batches, m, dev)
             kidx = torch.full((len(live),), n, dtype=torch.int32, device=dev)
-            ks = seal_setup(res_arena, kidx, pks, rng_key, 0, err)
+            ks = seal_setup(res_arena, kidx, pks, rng_key, 0, err).with_powers()
             ko = open_setup(res_arena, kidx, sks, pks, err)
             ev = torch.cuda.Event()
             ev.record(side)

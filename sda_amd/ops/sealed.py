@@ -126,8 +126,9 @@ def seal_setup(arena: Arena, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: 
 
     Independent of the message contents, so the engine runs it on a side stream
     concurrently with share generation. Writes epk into each slot header.
-    The Poly1305 chunk factors are left to :func:`seal_data` (a 30 us kernel on
-    the consuming stream), so the encrypt waits on the X25519 work only.
+    The Poly1305 tables come from :meth:`KeySet.with_powers` (the engine
+    derives them on its side stream right after this; :func:`seal_data` does
+    it on the consuming stream if they are missing).
     `gate`: (int32 tensor, token) posted when the kernel is dispatched.
     """
     keys = torch.empty(arena.M * G.MSGKEY_BYTES, dtype=torch.uint8, device=arena.ct.device)
