@@ -121,6 +121,8 @@ enum RngPurpose : uint64_t {
   kPurposeEphemeral = 6,
   kPurposeShares16 = 7,   // 16-bit share draws (two rows per ChaCha block)
   kPurposeRetry16 = 8,    // lane-private replacements for rejected 16-bit draws
+  kPurposeShares48 = 9,   // three draws per 32-bit word (m^3 < 2^32)
+  kPurposeRetry48 = 10,   // lane-private spare words for those
 };
 SDA_DEV uint64_t stream_id(uint64_t purpose, uint64_t owner) { return (purpose << 56) | owner; }
 

@@ -534,6 +534,166 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   }
 }
 
+// ---------------------------------- additive, three draws per 32-bit word ----
+// For m^3 < 2^32 (m <= 1625) one ChaCha word x yields three draws by Lemire's
+// multiply-shift: d0 = hi(x m), x1 = lo(x m), d1 = hi(x1 m), x2 = lo(x1 m),
+// d2 = hi(x2 m). Then d0 m^2 + d1 m + d2 = floor(x m^3 / 2^32) and lo(x m^3) is
+// the remainder, so rejecting x when lo(x m^3) < 2^32 mod m^3 leaves that floor
+// exactly uniform on [0, m^3): three independent exact-uniform draws per word,
+// 48 per ChaCha block (16-bit halves give 32) -- a third fewer ChaCha cores,
+// which are most of the kernel's VALU work, and 7 VALU ops per 3 draws instead
+// of a Barrett step per draw. A rejected word (1.7% at m = 433) is replaced by
+// the lane's next acceptable spare word (one private ChaCha block, screened
+// once), then by the per-word retry stream.
+// Layout: lane l of block b covers, per "triple" tt, elements l*16 .. +15 of
+// the three count tiles 3 (b kT3 + tt) + c; word i of a row's block gives
+// element i of each: digit c -> tile c.
+constexpr int kT3 = 3;  // triples per lane (9 count tiles per block)
+
+// An acceptable word (x m3 >= t3) from the per-word retry stream of `idx`.
+SDA_DEV uint32_t retry_word3(const RngKey& rk, uint64_t owner, uint64_t idx, uint32_t m3,
+                             uint32_t t3) {
+  for (uint64_t blk = 0;; ++blk) {
+    uint32_t w[16];
+    rng_block(w, rk, stream_id(kPurposeSharesRetry, owner), (idx << 8) | blk);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (w[i] * m3 >= t3) return w[i];
+  }
+}
+
+template <int MASK>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
+    k_share_additive48(int P, int D, int n, ModParams mp, uint32_t m3, uint32_t t3,
+                       const int32_t* __restrict__ secrets, RngKeyArg rng, uint64_t owner_base,
+                       uint16_t* __restrict__ shares, uint32_t* __restrict__ cnt,
+                       uint32_t* __restrict__ mask_out, uint32_t* __restrict__ mask_cnt) {
+  __shared__ uint32_t partial[kMaxRows16 + 1][3 * kT3][kWaves];
+  const int blk = blockIdx.x, p = blockIdx.y;
+  const int T = (D + kTileValues - 1) / kTileValues;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint64_t owner = owner_base + (uint64_t)p;
+  const RngKey rk = to_key(rng);
+  const uint32_t m = mp.m;
+  const u16x2 mm = {(uint16_t)m, (uint16_t)m};
+  const bool vec_ok = (D % 16) == 0;
+  constexpr int kMaskRows = MASK == kMaskFull ? 1 : 0;
+  const int rows = kMaskRows + (n - 1);
+  const uint64_t slots = (uint64_t)gridDim.x * kT3 * kBlock;  // (triple, lane) slots per row
+
+  // this lane's spare words (in LDS: dynamically indexed, and no registers
+  // held across the kernel); racc = the acceptable ones not used yet
+  __shared__ uint32_t spare[16][kBlock];
+  uint32_t racc = 0;
+  {
+    uint32_t rw[16];
+    rng_block(rw, rk, stream_id(kPurposeRetry48, owner), (uint64_t)blk * kBlock + tid);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      spare[k][tid] = rw[k];
+      racc |= (rw[k] * m3 >= t3 ? 1u : 0u) << k;
+    }
+  }
+  uint16_t* lastrow = shares + ((size_t)(n - 1) * P + p) * D;
+
+#pragma unroll 1
+  for (int tt = 0; tt < kT3; ++tt) {
+    int e0[3], valid[3];
+    uint32_t lastp[3][8];  // (masked) secrets becoming secret - sum(random shares), as pairs
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      e0[c] = blk * (3 * kT3 * kTileValues) + (3 * tt + c) * kTileValues + tid * 16;
+      valid[c] = max(0, min(16, D - e0[c]));
+      uint32_t s[16];
+      load16_secrets(s, secrets + (size_t)p * D + e0[c], valid[c], vec_ok, mp);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) lastp[c][k] = s[2 * k] | (s[2 * k + 1] << 16);
+    }
+    const uint64_t slot = ((uint64_t)blk * kT3 + tt) * kBlock + tid;
+    for (int r = 0; r < rows; ++r) {
+      uint32_t w[16];
+      rng_block(w, rk, stream_id(kPurposeShares48, owner), (uint64_t)r * slots + slot);
+      uint32_t rej = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) rej |= (w[k] * m3 < t3 ? 1u : 0u) << k;
+      if (__builtin_amdgcn_ballot_w64(rej != 0) != 0 && rej != 0) {
+        while (rej) {
+          const int b = __builtin_ctz(rej);
+          rej &= rej - 1;
+          uint32_t x;
+          if (racc) {
+            x = spare[__builtin_ctz(racc)][tid];
+            racc &= racc - 1;
+          } else {  // spares used up: exact draw from this word's retry stream
+            x = retry_word3(rk, owner, ((uint64_t)r << 40) | (slot * 16 + (uint64_t)b), m3, t3);
+          }
+#pragma unroll
+          for (int k = 0; k < 16; ++k) w[k] = k == b ? x : w[k];
+        }
+      }
+      // digit c of every word (hi(x m), then x <- lo(x m)), as u16 pairs -> tile c
+      const bool is_mask = r < kMaskRows;
+      uint32_t bytes[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        uint32_t vp[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) vp[k] = __umulhi(w[2 * k], m) | (__umulhi(w[2 * k + 1], m) << 16);
+        if (c < 2) {
+#pragma unroll
+          for (int k = 0; k < 16; ++k) w[k] *= m;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          lastp[c][k] = is_mask ? pk_add_mod(lastp[c][k], vp[k], mm) : pk_sub_mod(lastp[c][k], vp[k], mm);
+        bytes[c] = pairs_bytes<true>(vp, valid[c]);
+        if (is_mask) {
+          uint32_t v[16];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { v[2 * k] = vp[k] & 0xffffu; v[2 * k + 1] = vp[k] >> 16; }
+          store16<uint32_t>(mask_out + (size_t)p * D + e0[c], v, valid[c], vec_ok);
+        } else {
+          store_pairs(shares + ((size_t)(r - kMaskRows) * P + p) * D + e0[c], vp, valid[c], vec_ok);
+        }
+      }
+      const uint32_t b01 = wave_sum(bytes[0] | (bytes[1] << 16));  // each < 2^16
+      const uint32_t b2 = wave_sum(bytes[2]);
+      if (lane == 0) {
+        partial[r][3 * tt][wave] = b01 & 0xffffu;
+        partial[r][3 * tt + 1][wave] = b01 >> 16;
+        partial[r][3 * tt + 2][wave] = b2;
+      }
+    }
+    // the final shares of this triple
+    uint32_t lb[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      store_pairs(lastrow + e0[c], lastp[c], valid[c], vec_ok);
+      lb[c] = pairs_bytes<true>(lastp[c], valid[c]);
+    }
+    const uint32_t l01 = wave_sum(lb[0] | (lb[1] << 16));
+    const uint32_t l2 = wave_sum(lb[2]);
+    if (lane == 0) {
+      partial[kMaxRows16][3 * tt][wave] = l01 & 0xffffu;
+      partial[kMaxRows16][3 * tt + 1][wave] = l01 >> 16;
+      partial[kMaxRows16][3 * tt + 2][wave] = l2;
+    }
+  }
+  __syncthreads();
+  for (int x = tid; x < (rows + 1) * 3 * kT3; x += kBlock) {
+    const int r = x / (3 * kT3), g = x % (3 * kT3);
+    const int prow = r < rows ? r : kMaxRows16;
+    const int t = blk * 3 * kT3 + g;
+    if (t >= T) continue;
+    uint32_t s = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += partial[prow][g][w];
+    if (r < kMaskRows) mask_cnt[(size_t)p * T + t] = s;
+    else if (r < rows) cnt[((size_t)(r - kMaskRows) * P + p) * T + t] = s;
+    else cnt[((size_t)(n - 1) * P + p) * T + t] = s;
+  }
+}
+
 // --------------------------------------------------------- packed Shamir ----
 constexpr int kPssMaxK = 8;
 constexpr int kPssMaxT = 16;
@@ -717,6 +877,20 @@ void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, con
                        owner_base, seeds);
   // 16-bit draws: u16 shares, no ChaCha mask, room for the rows in LDS
   const bool rows_ok = (n - 1) + (mask_mode == kMaskFull ? 1 : 0) <= kMaxRows16;
+  const uint64_t m3 = (uint64_t)m * m * m;
+  if (g_share16 == 1 && value_bytes == 2 && m3 < (1ull << 32) && mask_mode != kMaskChaCha && rows_ok) {
+    const uint32_t t3 = (uint32_t)((1ull << 32) % m3);  // reject x with lo(x m^3) < t3
+    dim3 grid((D + 3 * kT3 * kTileValues - 1) / (3 * kT3 * kTileValues), P);
+    if (mask_mode == kMaskFull)
+      hipLaunchKernelGGL(k_share_additive48<kMaskFull>, grid, dim3(kBlock), 0, s, P, D, n, mp,
+                         (uint32_t)m3, t3, secrets, rng, owner_base, (uint16_t*)shares, cnt,
+                         mask_out, mask_cnt);
+    else
+      hipLaunchKernelGGL(k_share_additive48<kMaskNone>, grid, dim3(kBlock), 0, s, P, D, n, mp,
+                         (uint32_t)m3, t3, secrets, rng, owner_base, (uint16_t*)shares, cnt,
+                         mask_out, mask_cnt);
+    return;
+  }
   if (g_share16 && value_bytes == 2 && m <= 32768u && mask_mode != kMaskChaCha && rows_ok) {
     const uint32_t zone16 = 65536u - (65536u % m);
     dim3 grid((D + kGP * kTileValues - 1) / (kGP * kTileValues), P);

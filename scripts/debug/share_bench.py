@@ -7,8 +7,8 @@ x = torch.randint(0, m, (P, D), dtype=torch.int32, device="cuda")
 shares = torch.empty(n, P, D, dtype=torch.int16, device="cuda")
 cnt = torch.empty(n * P * G.tiles(D), dtype=torch.int32, device="cuda")
 err = torch.zeros(1, dtype=torch.int32, device="cuda")
-names = {0: "share32", 1: "share16"}
-for mode in (0, 1, 0, 1):
+names = {0: "share32", 1: "share48 (3 draws/word)", 2: "share16 (u16 halves)"}
+for mode in (0, 1, 2, 1, 2):
     gpu().set_share16(mode)
     for _ in range(2):
         G.share_additive(x, n, m, shares, cnt, G.MASK_NONE, bytes(32), 0, err=err)

@@ -38,17 +38,24 @@ def _run(m, n, P, D, mask):
     return sh
 
 
-@pytest.mark.parametrize("m", [433, 40000, 65521, 2, 8192, 8193, 20000, 32768])
+# m^3 < 2^32 (m <= 1625) takes the three-draws-per-word kernel (1291: ~50% of the
+# words rejected, so spare and retry-stream replacements run constantly)
+@pytest.mark.parametrize("m", [433, 40000, 65521, 2, 3, 1000, 1291, 1625, 1626, 8192, 8193, 20000,
+                               32768])
 @pytest.mark.parametrize("n,mask", [(3, False), (2, True), (5, True), (8, False)])
 def test_share16_exact(cuda, m, n, mask):
     _run(m, n, 3, 70001, mask)  # D not a multiple of the 16384-element block
 
 
-def test_share16_uniform_under_rejection(cuda):
-    m = 40000
+@pytest.mark.parametrize("m", [40000, 1291, 433])
+def test_share16_uniform_under_rejection(cuda, m):
     sh = _run(m, 3, 16, 200000, False)
-    row = sh[0].reshape(-1).float()
-    buckets = torch.histc(row, bins=20, min=0, max=m)
-    expected = row.numel() / 20
-    chi2 = float(((buckets - expected) ** 2 / expected).sum())
-    assert chi2 < 60, chi2  # 19 degrees of freedom; p < 1e-5 beyond ~50
+    for r in range(2):  # both random rows (the third is secret - their sum)
+        row = sh[r].reshape(-1)
+        if m > 4096:  # 20 equal-width buckets (m = 40000: 2000 values each)
+            counts, dof = torch.histc(row.float(), bins=20, min=0, max=m), 19
+        else:  # every residue
+            counts, dof = torch.bincount(row, minlength=m).double(), m - 1
+        expected = row.numel() / counts.numel()
+        chi2 = float(((counts - expected) ** 2 / expected).sum())
+        assert chi2 < dof + 6 * (2 * dof) ** 0.5, (m, r, chi2)
