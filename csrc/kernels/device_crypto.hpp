@@ -123,6 +123,7 @@ enum RngPurpose : uint64_t {
   kPurposeRetry16 = 8,    // lane-private replacements for rejected 16-bit draws
   kPurposeShares48 = 9,   // three draws per 32-bit word (m^3 < 2^32)
   kPurposeRetry48 = 10,   // lane-private spare words for those
+  kPurposeSharesPss48 = 11,  // packed-Shamir randomness, three draws per word
 };
 SDA_DEV uint64_t stream_id(uint64_t purpose, uint64_t owner) { return (purpose << 56) | owner; }
 

@@ -116,6 +116,7 @@ PYBIND11_MODULE(_sda_gpu, m) {
         });
   m.def("set_share16", &set_share16, "use the 16-bit-draw additive share kernel (benchmarking)");
   m.def("set_key_prio", &set_key_prio, "wave priority of open setup / Poly1305 tables (1 = top)");
+  m.def("set_pss48", &set_pss48, "packed-Shamir small-field share kernel (benchmarking)");
   m.def("set_mac_mfma", &set_mac_mfma, "matrix-core Poly1305 segments (benchmarking; 0 = Horner)");
   m.def("count", [](int M, int L, int value_bytes, uintptr_t vals, uintptr_t cnt, uintptr_t stream) {
     launch_count(M, L, value_bytes, P<const void>(vals), P<uint32_t>(cnt), S(stream));

@@ -95,8 +95,12 @@ void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, con
                            void* shares, uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt,
                            uint32_t* seeds, uint32_t* err, hipStream_t s);
 
-// Select the 16-bit-draw additive kernel (default on) -- benchmarking switch.
+// Additive share kernel selection -- benchmarking switch: 1 (default) = three
+// draws per word where m^3 < 2^32, else 16-bit halves; 2 = 16-bit halves; 0 = u32.
 void set_share16(int mode);
+// Packed-Shamir small-field kernel (k = 3, n = 8, t = 2 or 4, no mask; default
+// on) -- benchmarking switch.
+void set_pss48(int mode);
 
 // Packed Shamir: shares = M . [s_1..s_k, r_1..r_t] mod p per batch (M: n x (k+t)
 // host-computed from the tss FFT construction).

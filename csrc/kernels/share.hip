@@ -815,6 +815,132 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+// ------------------------------------- packed Shamir, small fields (VALU) ----
+// The reference parameter sets with n = 8 clerks and k = 3 secrets per batch
+// (PSS_4_8_3 and the 5-of-8 set, t = 4 / 2) over p = 433: shares = M [s; r] per
+// batch with u32 accumulation (K (p-1)^2 < 2^32: 24-bit multiply-adds) and one
+// Barrett step per share. The t field elements of randomness of 32 / t batches
+// come from one ChaCha block as Lemire triples (11 of its 16 words; rejected
+// words are replaced by its other 5, then by the per-word retry stream) --
+// where k_share_pss spends a whole block on every batch. Thread i of block b
+// handles batches b * 4096 + i + 256 g, g < 16 (count tile b; consecutive lanes
+// store consecutive u16 shares). M is staged in LDS with rows padded to 8, read
+// as two broadcast 16-byte loads per clerk.
+constexpr int kPssKS = 3;  // secrets per batch
+constexpr int kPssNC = 8;  // clerks
+
+template <int T>
+__global__ void __launch_bounds__(kBlock)
+    k_share_pss48(int P, int D, ModParams mp, uint32_t m3, uint32_t t3,
+                  const int32_t* __restrict__ secrets, const uint32_t* __restrict__ mat,
+                  RngKeyArg rng, uint64_t owner_base, uint16_t* __restrict__ shares,
+                  uint32_t* __restrict__ cnt) {
+  constexpr int K = kPssKS + T;
+  constexpr int kPerBlock = 32 / T;      // batches per ChaCha block
+  constexpr int kRounds = 16 / kPerBlock;
+  __shared__ __attribute__((aligned(16))) uint32_t sM[kPssNC][8];
+  __shared__ uint32_t partial[kPssNC][kWaves];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid < kPssNC * 8) sM[tid >> 3][tid & 7] = (tid & 7) < K ? mat[(tid >> 3) * K + (tid & 7)] : 0u;
+  __syncthreads();
+  const int tile = blockIdx.x, p = blockIdx.y, Tt = gridDim.x;
+  const int B = (D + kPssKS - 1) / kPssKS;
+  const uint64_t owner = owner_base + (uint64_t)p;
+  const RngKey rk = to_key(rng);
+  const uint32_t m = mp.m;
+  uint32_t extra[kPssNC];  // per clerk: shares of two varint bytes (v >= 64)
+#pragma unroll
+  for (int c = 0; c < kPssNC; ++c) extra[c] = 0;
+  uint32_t nvalid = 0;
+
+#pragma unroll 1
+  for (int rd = 0; rd < kRounds; ++rd) {
+    uint32_t w[16];
+    const uint64_t ctr = ((uint64_t)tile * kBlock + tid) * kRounds + rd;
+    rng_block(w, rk, stream_id(kPurposeSharesPss48, owner), ctr);
+    uint32_t rej = 0, spare = 0;
+#pragma unroll
+    for (int i = 0; i < 11; ++i) rej |= (w[i] * m3 < t3 ? 1u : 0u) << i;
+#pragma unroll
+    for (int i = 11; i < 16; ++i) spare |= (w[i] * m3 >= t3 ? 1u : 0u) << i;
+    if (__builtin_amdgcn_ballot_w64(rej != 0) != 0 && rej != 0) {
+      while (rej) {
+        const int bi = __builtin_ctz(rej);
+        rej &= rej - 1;
+        uint32_t x;
+        if (spare) {
+          const int si = __builtin_ctz(spare);
+          spare &= spare - 1;
+          x = 0;
+#pragma unroll
+          for (int i = 11; i < 16; ++i) x = i == si ? w[i] : x;
+        } else {
+          x = retry_word3(rk, owner, (ctr << 4) | (uint64_t)bi, m3, t3);
+        }
+#pragma unroll
+        for (int i = 0; i < 11; ++i) w[i] = i == bi ? x : w[i];
+      }
+    }
+    uint32_t dg[33];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) {
+      const uint32_t x0 = w[i], x1 = x0 * m;
+      dg[3 * i] = __umulhi(x0, m);
+      dg[3 * i + 1] = __umulhi(x1, m);
+      dg[3 * i + 2] = __umulhi(x1 * m, m);
+    }
+    // this round's batches: secrets (canonical) and randomness
+    uint32_t s[kPerBlock][kPssKS];
+    bool ok[kPerBlock];
+    int bidx[kPerBlock];
+#pragma unroll
+    for (int g = 0; g < kPerBlock; ++g) {
+      const int b = tile * kTileValues + tid + kBlock * (rd * kPerBlock + g);
+      bidx[g] = b;
+      ok[g] = b < B;
+#pragma unroll
+      for (int j = 0; j < kPssKS; ++j) {
+        const int e = b * kPssKS + j;
+        s[g][j] = (ok[g] && e < D) ? canon_i32(secrets[(size_t)p * D + e], mp) : 0u;
+      }
+      nvalid += ok[g] ? 1u : 0u;
+    }
+#pragma unroll
+    for (int c = 0; c < kPssNC; ++c) {
+      const uint4 m0 = *reinterpret_cast<const uint4*>(&sM[c][0]);
+      const uint4 m1 = *reinterpret_cast<const uint4*>(&sM[c][4]);
+      const uint32_t row[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+      uint16_t* out = shares + ((size_t)c * P + p) * B;
+#pragma unroll
+      for (int g = 0; g < kPerBlock; ++g) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < kPssKS; ++j) acc += __umul24(row[j], s[g][j]);
+#pragma unroll
+        for (int d = 0; d < T; ++d) acc += __umul24(row[kPssKS + d], dg[g * T + d]);
+        const uint32_t y = mod32(acc, mp);
+        if (ok[g]) {
+          out[bidx[g]] = (uint16_t)y;
+          extra[c] += y >= 64u ? 1u : 0u;
+        }
+      }
+    }
+  }
+  // per-clerk tile byte counts: one byte per share, two for v >= 64 (p <= 8192)
+#pragma unroll
+  for (int c = 0; c < kPssNC; ++c) {
+    const uint32_t v = wave_sum(nvalid + extra[c]);
+    if (lane == 0) partial[c][wave] = v;
+  }
+  __syncthreads();
+  if (tid < kPssNC) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) v += partial[tid][w];
+    cnt[((size_t)tid * P + p) * Tt + tile] = v;
+  }
+}
+
 // ----------------------------------------------------------------- count ---
 template <typename VT>
 __global__ void __launch_bounds__(kBlock) k_count(int L, const VT* __restrict__ vals,
@@ -864,6 +990,8 @@ __global__ void __launch_bounds__(kBlock)
 
 static int g_share16 = 1;
 void set_share16(int mode) { g_share16 = mode; }
+static int g_pss48 = 1;
+void set_pss48(int mode) { g_pss48 = mode; }
 
 void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, const int32_t* secrets,
                            int mask_mode, int seed_words, RngKeyArg rng, uint64_t owner_base,
@@ -950,7 +1078,19 @@ void launch_share_pss(int P, int D, int n, int k, int t, uint32_t p, int value_b
     hipLaunchKernelGGL(k_chacha_seeds, dim3((P + 63) / 64), dim3(64), 0, s, P, seed_words, rng,
                        owner_base, seeds);
   dim3 grid((B + kTileValues - 1) / kTileValues, P);
-#define SDA_PSS_LAUNCH(VT, MK)                                                                \
+  const uint64_t p3 = (uint64_t)p * p * p;
+  if (g_pss48 && value_bytes == 2 && mask_mode == kMaskNone && k == kPssKS && n == kPssNC &&
+      (t == 2 || t == 4) && p <= 8192u && p3 < (1ull << 32)) {
+    const uint32_t t3 = (uint32_t)((1ull << 32) % p3);
+    if (t == 4)
+      hipLaunchKernelGGL(k_share_pss48<4>, grid, dim3(kBlock), 0, s, P, D, mp, (uint32_t)p3, t3,
+                         secrets, share_matrix, rng, owner_base, (uint16_t*)shares, cnt);
+    else
+      hipLaunchKernelGGL(k_share_pss48<2>, grid, dim3(kBlock), 0, s, P, D, mp, (uint32_t)p3, t3,
+                         secrets, share_matrix, rng, owner_base, (uint16_t*)shares, cnt);
+    return;
+  }
+#define SDA_PSS_LAUNCH(VT, MK)                                                             \
   hipLaunchKernelGGL((k_share_pss<VT, MK>), grid, dim3(kBlock), 0, s, P, D, n, k, t, mp,       \
                      small_acc, secrets, share_matrix, rng, owner_base, (VT*)shares, cnt,      \
                      mask_out, mask_cnt, seeds, seed_words, err)
