@@ -14,11 +14,16 @@ time (whole job: summed over all ranks).
 
 Scaling is *weak*: each rank hosts `--participants` (default 1000) participants,
 so N ranks aggregate N x 1000 x 1M elements per step. With N > 1 the round runs
-through sda_amd.parallel.DistributedAggregator: by default the committee layout
-(each rank seals its participants' boxes; the snapshot transpose routes them
-over xGMI to the ranks playing the clerks, with no rank holding two clerks'
-shares of a participant; clerk partial sums are reduced to rank 0, the
-recipient). `--layout owner` skips the routing (upper bound).
+through sda_amd.parallel.DistributedAggregator. Default layout `owner`: every
+GPU hosts a slice of each of the n clerks (a clerk is one organisation whose job
+spans the node), so a GPU opens the boxes its own participants sealed -- the
+same per-GPU trust boundary as the one-GPU round -- and the clerks' partial sums
+plus mask partials are reduced to rank 0, the recipient, in one RCCL bucket:
+N x the one-GPU work, (n+1) x D integers over xGMI per round.
+`--layout committee` routes every sealed box over xGMI to ranks playing the
+clerks (no rank holding two clerks' shares of a participant): the snapshot
+transpose as grouped RCCL send/recv, 5.5 GB out of every rank per round, which
+a point-to-point xGMI link cannot move in one round's compute time at N=2.
 
 Launch: python bench.py --gpus 1 --steps 5 --warmup 2
         python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -61,9 +66,10 @@ def parse():
     ap.add_argument("--modulus", type=int, default=433)
     ap.add_argument("--check", action="store_true", help="verify the output every step")
     ap.add_argument("--stages", action="store_true", help="print per-stage times (rank 0)")
-    ap.add_argument("--layout", default="committee", choices=["committee", "owner"],
+    ap.add_argument("--layout", default="owner", choices=["committee", "owner"],
                     help="committee: boxes routed to the clerks' GPUs (protocol trust model); "
-                         "owner: each GPU opens its own participants' boxes (upper bound)")
+                         "owner: each GPU hosts a slice of every clerk and opens its own "
+                         "participants' boxes (default)")
     ap.add_argument("--waves", type=int, default=4,
                     help="committee layout: participant waves the exchange is pipelined over")
     ap.add_argument("--force-dist", action="store_true",
@@ -182,7 +188,8 @@ def main():
                 "parallelism": (f"dp{world} participants x committee-sharded clerks: sealed "
                                 "boxes routed over xGMI (grouped RCCL send/recv), clerk partials "
                                 "reduced to rank 0" if args.layout == "committee" else
-                                f"dp{world} owner-computes: clerk partials reduced to rank 0")
+                                f"dp{world} participants, every GPU hosting a slice of each clerk: clerk "
+                                "partials + mask partials reduced to rank 0 over RCCL")
                                if world > 1 else "single GPU",
             },
         }
