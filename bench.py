@@ -37,12 +37,6 @@ import os
 import sys
 import time
 
-# RCCL (one stream per P2P peer) + the engine's side stream need more than the
-# default 4 hardware queues per process, or streams get multiplexed onto one
-# queue and serialise (measured: +6 ms per round). Must precede HIP init.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
@@ -74,6 +68,8 @@ def parse():
                     help="committee layout: participant waves the exchange is pipelined over")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the distributed engine even on one rank (measures its overhead)")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="override GPU_MAX_HW_QUEUES (0 = leave the process default)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU")
     return ap.parse_args()
@@ -81,6 +77,8 @@ def parse():
 
 def main():
     args = parse()
+    if args.hw_queues > 0:  # must precede HIP init
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
     import torch
     import torch.distributed as dist
 

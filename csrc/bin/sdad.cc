@@ -28,7 +28,7 @@ void on_signal(int) { g_stop = 1; }
   if (!why.empty()) std::fprintf(stderr, "error: %s\n\n", why.c_str());
   std::fprintf(stderr,
                "usage: sdad [-v...] (--jfs DIR | --document DIR | --memory) httpd "
-               "[-b IP:PORT] [--threads N]\n"
+               "[-b IP:PORT] [--threads N] [--max-body-mb N]\n"
                "  httpd   run the REST server (default bind 127.0.0.1:8888)\n");
   std::exit(2);
 }
@@ -39,6 +39,7 @@ int main(int argc, char** argv) {
   std::string jfs, doc, mongo, bind = "127.0.0.1:8888", sub;
   bool memory = false;
   int verbose = 0, threads = 8;
+  size_t max_body_mb = 256;
   for (int i = 1; i < argc; ++i) {
     std::string s = argv[i];
     auto val = [&](const char* what) -> std::string {
@@ -53,6 +54,7 @@ int main(int argc, char** argv) {
     else if (s == "--memory") memory = true;
     else if (s == "-b" || s == "--bind") bind = val("--bind");
     else if (s == "--threads") threads = std::stoi(val("--threads"));
+    else if (s == "--max-body-mb") max_body_mb = std::stoul(val("--max-body-mb"));
     else if (s.size() > 1 && s[0] == '-' && s.find_first_not_of('v', 1) == std::string::npos)
       verbose += (int)s.size() - 1;
     else if (s == "--verbose") ++verbose;
@@ -71,6 +73,7 @@ int main(int argc, char** argv) {
     if (sub != "httpd") throw SdaError("Unknown subcommand");
     auto handler = std::make_shared<SdaHttpHandler>(svc);
     HttpServer server([handler](const HttpRequest& r) { return handler->handle(r); }, threads);
+    server.set_max_body(max_body_mb << 20);
     const int port = server.start(bind);
     log_info("Starting server on " + bind + " (port " + std::to_string(port) + ")");
     std::printf("listening on port %d\n", port);

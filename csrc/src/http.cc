@@ -67,17 +67,37 @@ const char* reason(int code) {
   }
 }
 
-// Read one HTTP message (request or response) head + body from fd.
-// Returns false on EOF / error. `buf` may hold bytes of a following message.
-bool read_message(int fd, std::string& buf, std::string& head, std::string& body,
-                  bool is_response, size_t max_body = (size_t)8 << 30) {
+// Strict unsigned parse (digits of `base` only, no sign / whitespace / overflow).
+bool parse_uint(const std::string& s, int base, size_t& out) {
+  if (s.empty() || s.size() > 16) return false;
+  size_t v = 0;
+  for (char c : s) {
+    int d;
+    if (c >= '0' && c <= '9') d = c - '0';
+    else if (base == 16 && c >= 'a' && c <= 'f') d = c - 'a' + 10;
+    else if (base == 16 && c >= 'A' && c <= 'F') d = c - 'A' + 10;
+    else return false;
+    if (v > (SIZE_MAX - (size_t)d) / (size_t)base) return false;
+    v = v * (size_t)base + (size_t)d;
+  }
+  out = v;
+  return true;
+}
+
+enum class ReadStatus { Ok, Closed, Malformed, TooLarge };
+
+// Read one HTTP message (request or response) head + body from fd. `buf` may
+// hold bytes of a following message. Never throws: a peer can make it return
+// Malformed / TooLarge, nothing else.
+ReadStatus read_message(int fd, std::string& buf, std::string& head, std::string& body,
+                        bool is_response, size_t max_body) {
   size_t hdr_end;
   while ((hdr_end = buf.find("\r\n\r\n")) == std::string::npos) {
-    if (buf.size() > (1 << 20)) return false;
+    if (buf.size() > (1 << 20)) return ReadStatus::Malformed;
     char tmp[65536];
     ssize_t r = ::recv(fd, tmp, sizeof(tmp), 0);
     if (r < 0 && errno == EINTR) continue;
-    if (r <= 0) return false;
+    if (r <= 0) return ReadStatus::Closed;
     buf.append(tmp, (size_t)r);
   }
   head = buf.substr(0, hdr_end);
@@ -88,7 +108,7 @@ bool read_message(int fd, std::string& buf, std::string& head, std::string& body
   for (auto& line : split(lh, '\n')) {
     auto l = trim(line);
     if (l.rfind("content-length:", 0) == 0) {
-      clen = std::stoull(trim(l.substr(15)));
+      if (!parse_uint(trim(l.substr(15)), 10, clen)) return ReadStatus::Malformed;
       has_len = true;
     } else if (l.rfind("transfer-encoding:", 0) == 0 && l.find("chunked") != std::string::npos) {
       chunked = true;
@@ -108,19 +128,27 @@ bool read_message(int fd, std::string& buf, std::string& head, std::string& body
   if (chunked) {
     while (true) {
       size_t eol;
-      while ((eol = buf.find("\r\n")) == std::string::npos)
-        if (!fill(buf.size() + 1)) return false;
-      size_t n = std::stoull(buf.substr(0, eol), nullptr, 16);
+      while ((eol = buf.find("\r\n")) == std::string::npos) {
+        if (buf.size() > 4096) return ReadStatus::Malformed;  // a chunk-size line is short
+        if (!fill(buf.size() + 1)) return ReadStatus::Closed;
+      }
+      std::string size_field = buf.substr(0, eol);
+      auto ext = size_field.find(';');  // chunk extensions are ignored
+      if (ext != std::string::npos) size_field.resize(ext);
+      size_t n;
+      if (!parse_uint(trim(size_field), 16, n)) return ReadStatus::Malformed;
+      // the budget is checked before anything of the chunk is buffered
+      if (n > max_body || body.size() > max_body - n) return ReadStatus::TooLarge;
       buf.erase(0, eol + 2);
-      if (!fill(n + 2)) return false;
+      if (!fill(n + 2)) return ReadStatus::Closed;
+      if (buf[n] != '\r' || buf[n + 1] != '\n') return ReadStatus::Malformed;
       body.append(buf, 0, n);
       buf.erase(0, n + 2);
       if (n == 0) break;
-      if (body.size() > max_body) return false;
     }
   } else if (has_len) {
-    if (clen > max_body) return false;
-    if (!fill(clen)) return false;
+    if (clen > max_body) return ReadStatus::TooLarge;
+    if (!fill(clen)) return ReadStatus::Closed;
     body = buf.substr(0, clen);
     buf.erase(0, clen);
   } else if (is_response) {
@@ -130,10 +158,11 @@ bool read_message(int fd, std::string& buf, std::string& head, std::string& body
       if (r < 0 && errno == EINTR) continue;
       if (r <= 0) break;
       buf.append(tmp, (size_t)r);
+      if (buf.size() > max_body) return ReadStatus::TooLarge;
     }
     body.swap(buf);
   }
-  return true;
+  return ReadStatus::Ok;
 }
 
 }  // namespace
@@ -146,8 +175,11 @@ std::string HttpRequest::header(const std::string& n) const {
 std::string url_decode(const std::string& s) {
   std::string out;
   for (size_t i = 0; i < s.size(); ++i) {
-    if (s[i] == '%' && i + 2 < s.size()) {
-      out.push_back((char)std::stoi(s.substr(i + 1, 2), nullptr, 16));
+    if (s[i] == '%') {
+      size_t v;
+      if (i + 3 > s.size() || !parse_uint(s.substr(i + 1, 2), 16, v))
+        throw SdaError(ErrorKind::Invalid, "malformed %-escape in URL");
+      out.push_back((char)v);
       i += 2;
     } else if (s[i] == '+') {
       out.push_back(' ');
@@ -240,7 +272,11 @@ void HttpServer::worker_loop() {
       fd = q_->fds.front();
       q_->fds.pop_front();
     }
-    handle_conn(fd);
+    try {
+      handle_conn(fd);
+    } catch (...) {
+      // a worker never dies with its connection
+    }
     ::close(fd);
   }
 }
@@ -251,38 +287,62 @@ void HttpServer::handle_conn(int fd) {
     std::string head, body;
     pollfd p{fd, POLLIN, 0};
     if (buf.empty() && ::poll(&p, 1, 30000) <= 0) return;  // idle keep-alive timeout
-    if (!read_message(fd, buf, head, body, false)) return;
+    const ReadStatus rs = read_message(fd, buf, head, body, false, max_body_);
+    if (rs == ReadStatus::Closed) return;
     HttpRequest req;
-    auto lines = split(head, '\n');
-    auto rl = split(trim(lines[0]), ' ');
-    if (rl.size() < 2) return;
-    req.method = rl[0];
-    req.target = rl[1];
-    auto qpos = req.target.find('?');
-    req.path = qpos == std::string::npos ? req.target : req.target.substr(0, qpos);
-    if (qpos != std::string::npos) {
-      for (auto& kv : split(req.target.substr(qpos + 1), '&')) {
-        auto eq = kv.find('=');
-        if (eq == std::string::npos) req.query[url_decode(kv)] = "";
-        else req.query[url_decode(kv.substr(0, eq))] = url_decode(kv.substr(eq + 1));
+    HttpResponse resp;
+    bool keep_alive = false;
+    // Nothing a peer sends may escape as an exception: a malformed request is
+    // answered with 400 (413 for an oversized body) and the connection closed.
+    bool parsed = false;
+    if (rs == ReadStatus::Ok) {
+      try {
+        auto lines = split(head, '\n');
+        auto rl = split(trim(lines.at(0)), ' ');
+        if (rl.size() < 2) throw SdaError(ErrorKind::Invalid, "malformed request line");
+        req.method = rl[0];
+        req.target = rl[1];
+        auto qpos = req.target.find('?');
+        req.path = qpos == std::string::npos ? req.target : req.target.substr(0, qpos);
+        if (qpos != std::string::npos) {
+          for (auto& kv : split(req.target.substr(qpos + 1), '&')) {
+            auto eq = kv.find('=');
+            if (eq == std::string::npos) req.query[url_decode(kv)] = "";
+            else req.query[url_decode(kv.substr(0, eq))] = url_decode(kv.substr(eq + 1));
+          }
+        }
+        keep_alive = rl.size() >= 3 && rl[2].find("1.1") != std::string::npos;
+        for (size_t i = 1; i < lines.size(); ++i) {
+          auto c = lines[i].find(':');
+          if (c == std::string::npos) continue;
+          req.headers[lower(trim(lines[i].substr(0, c)))] = trim(lines[i].substr(c + 1));
+        }
+        if (lower(req.header("connection")) == "close") keep_alive = false;
+        if (lower(req.header("connection")) == "keep-alive") keep_alive = true;
+        req.body = std::move(body);
+        parsed = true;
+      } catch (const std::exception& e) {
+        resp.body = e.what();
       }
     }
-    bool keep_alive = rl.size() >= 3 && rl[2].find("1.1") != std::string::npos;
-    for (size_t i = 1; i < lines.size(); ++i) {
-      auto c = lines[i].find(':');
-      if (c == std::string::npos) continue;
-      req.headers[lower(trim(lines[i].substr(0, c)))] = trim(lines[i].substr(c + 1));
-    }
-    if (lower(req.header("connection")) == "close") keep_alive = false;
-    if (lower(req.header("connection")) == "keep-alive") keep_alive = true;
-    req.body = std::move(body);
-    HttpResponse resp;
-    try {
-      resp = handler_(req);
-    } catch (const std::exception& e) {
-      resp.status = 500;
+    if (!parsed) {
+      resp.status = rs == ReadStatus::TooLarge ? 413 : 400;
       resp.content_type = "text/plain; charset=utf-8";
-      resp.body = e.what();
+      if (resp.body.empty())
+        resp.body = rs == ReadStatus::TooLarge ? "request body too large" : "malformed HTTP request";
+      keep_alive = false;  // the stream position is unknown after a bad message
+    } else {
+      try {
+        resp = handler_(req);
+      } catch (const std::exception& e) {
+        resp.status = 500;
+        resp.content_type = "text/plain; charset=utf-8";
+        resp.body = e.what();
+      } catch (...) {
+        resp.status = 500;
+        resp.content_type = "text/plain; charset=utf-8";
+        resp.body = "internal error";
+      }
     }
     std::ostringstream out;
     out << "HTTP/1.1 " << resp.status << " " << reason(resp.status) << "\r\n";
@@ -541,7 +601,7 @@ SdaHttpClient::Reply SdaHttpClient::request(const std::string& method, const std
             (!json_body || send_all(fd, json_body->data(), json_body->size()));
   Reply rep;
   std::string buf, rhead;
-  if (!ok || !read_message(fd, buf, rhead, rep.body, true)) {
+  if (!ok || read_message(fd, buf, rhead, rep.body, true, (size_t)8 << 30) != ReadStatus::Ok) {
     ::close(fd);
     throw SdaError("HTTP/REST error: connection failed");
   }

@@ -188,9 +188,9 @@ class DeviceAggregator:
 
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
-            # high priority: its kernels are latency-bound X25519 ladders with few
-            # waves, which must not queue behind the main stream's full-chip grids
-            self._side = torch.cuda.Stream(device=self.device, priority=-1)
+            # default priority, like every stream of the process: its kernels are
+            # latency-bound X25519 ladders that raise their own wave priority
+            self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
     def _live(self, clerks):

@@ -105,3 +105,76 @@ def test_agent_create_is_idempotent(sdad, tmp_path):
     # keys show lists what keys create made
     kid = _sda(sdad, ident, "agent", "keys", "create").stdout.strip()
     assert kid in _sda(sdad, ident, "agent", "keys", "show").stdout.split()
+
+
+# ---- hostile HTTP input against the real daemon ------------------------------------
+def _raw(server, payload: bytes, read=True) -> bytes:
+    import socket
+
+    host, port = server[len("http://"):].split(":")
+    with socket.create_connection((host, int(port)), timeout=10) as s:
+        s.sendall(payload)
+        if not read:
+            return b""
+        s.settimeout(10)
+        chunks = []
+        try:
+            while True:
+                b = s.recv(65536)
+                if not b:
+                    break
+                chunks.append(b)
+        except OSError:
+            pass
+        return b"".join(chunks)
+
+
+def _ping_ok(server):
+    rep = _raw(server, b"GET /v1/ping HTTP/1.1\r\nConnection: close\r\n\r\n")
+    return rep.startswith(b"HTTP/1.1 200") and b'{"running":true}' in rep
+
+
+@pytest.mark.parametrize("payload,status", [
+    (b"POST /v1/agents/me HTTP/1.1\r\nContent-Length: abc\r\n\r\n", b"400"),
+    (b"POST /v1/agents/me HTTP/1.1\r\nContent-Length: -1\r\n\r\n", b"400"),
+    (b"POST /v1/agents/me HTTP/1.1\r\nContent-Length: 99999999999999999999999\r\n\r\n", b"400"),
+    (b"GET /v1/ping?a=%zz HTTP/1.1\r\n\r\n", b"400"),
+    (b"GET /v1/ping?a=%4 HTTP/1.1\r\n\r\n", b"400"),
+    (b"POST /v1/agents/me HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\nzz\r\n", b"400"),
+    (b"POST /v1/agents/me HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\nffffffffffffffff\r\n", b"413"),
+    (b"POST /v1/agents/me HTTP/1.1\r\nContent-Length: 999999999999\r\n\r\n", b"413"),
+    (b"\r\n\r\n", b"400"),
+])
+def test_daemon_survives_malformed_requests(sdad, payload, status):
+    """Unauthenticated garbage is answered (400 / 413), never fatal: the
+    reference server answers such requests with an error too (rouille;
+    server-http/src/lib.rs:105-122)."""
+    rep = _raw(sdad, payload)
+    assert rep.startswith(b"HTTP/1.1 " + status), rep[:200]
+    assert _ping_ok(sdad)
+
+
+def test_daemon_enforces_body_budget(tmp_path, native):
+    """--max-body-mb bounds request bodies before they are buffered."""
+    exe = bin_path("sdad")
+    port = _free_port()
+    proc = subprocess.Popen([exe, "--memory", "httpd", "-b", f"127.0.0.1:{port}",
+                             "--max-body-mb", "1"], stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE, text=True)
+    try:
+        assert "listening" in proc.stdout.readline()
+        server = f"http://127.0.0.1:{port}"
+        rep = _raw(server, b"POST /v1/agents/me HTTP/1.1\r\nContent-Length: 2000000\r\n\r\n")
+        assert rep.startswith(b"HTTP/1.1 413"), rep[:200]
+        # chunked: the declared chunk alone exceeds the budget
+        rep = _raw(server, b"POST /v1/agents/me HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n"
+                           b"200000\r\n")
+        assert rep.startswith(b"HTTP/1.1 413"), rep[:200]
+        assert _ping_ok(server)
+    finally:
+        proc.send_signal(signal.SIGTERM)
+        try:
+            proc.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+            proc.wait()
