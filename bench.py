@@ -8,22 +8,20 @@ participants, 3 clerks)" -- config 2: 1000 participants x 1,000,000-dim vectors,
 One *step* is a complete SDA round, end to end on device: participants mask +
 share + seal (X25519 / XSalsa20-Poly1305) their vectors for every clerk, shares
 are routed to the clerks, every clerk verifies + decrypts + decodes + combines
-its P boxes and seals the sum for the recipient, the recipient opens the n
+its boxes and seals the sum for the recipient, the recipient opens the n
 results, reconstructs and unmasks. elements/s = participants x dimension / step
-time (whole job: summed over all ranks).
+time (whole job: summed over all ranks). Every step draws fresh keys and
+randomness; nothing is cached between steps.
 
 Scaling is *weak*: each rank hosts `--participants` (default 1000) participants,
 so N ranks aggregate N x 1000 x 1M elements per step. With N > 1 the round runs
-through sda_amd.parallel.DistributedAggregator. Default layout `owner`: every
-GPU hosts a slice of each of the n clerks (a clerk is one organisation whose job
-spans the node), so a GPU opens the boxes its own participants sealed -- the
-same per-GPU trust boundary as the one-GPU round -- and the clerks' partial sums
-plus mask partials are reduced to rank 0, the recipient, in one RCCL bucket:
-N x the one-GPU work, (n+1) x D integers over xGMI per round.
-`--layout committee` routes every sealed box over xGMI to ranks playing the
-clerks (no rank holding two clerks' shares of a participant): the snapshot
-transpose as grouped RCCL send/recv, 5.5 GB out of every rank per round, which
-a point-to-point xGMI link cannot move in one round's compute time at N=2.
+through sda_amd.parallel.DistributedAggregator in its `committee` layout, the
+protocol's trust model: every sealed box crosses xGMI to a rank that plays its
+clerk (a uniform all-to-all, ~5.5 GB out of every rank per round at the default
+size), each rank holds only its own clerks' secret keys, clerks' combined
+shares reach rank 0 -- the recipient -- sealed. `--layout owner` is an explicit
+non-private upper bound (each GPU opens its own participants' boxes and the
+plaintext partial sums are reduced): it shows what the all-to-all costs.
 
 Launch: python bench.py --gpus 1 --steps 5 --warmup 2
         python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -32,6 +30,7 @@ Launch: python bench.py --gpus 1 --steps 5 --warmup 2
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -42,11 +41,34 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 METRIC = "aggregated secret-shared elements/sec (1M-dim vec, 1k participants, 3 clerks)"
-# Reference-equivalent single-threaded CPU implementation, measured here (the
-# reference publishes no numbers): `sda_cpu_bench --participants 4
-# --dim 1000000` -> 1.16e6 elements/s (OS-RNG draw per share value, sealed box
-# per (participant, clerk), element-wise combine), same 3-clerk mod-433 config.
-BASELINE_ELEMS_PER_S = 1.16e6
+# The reference publishes no numbers (BASELINE.json "published": {}), so the
+# denominators are reference-equivalent CPU implementations measured here with
+# `sda_cpu_bench` on the same 3-clerk mod-433 1M-dim config:
+#   strongest point  -- 8 threads, buffered ChaCha20 RNG:          1.41e7 elements/s
+#   reference-style  -- 1 thread, one OS-RNG draw per share value: 1.16e6 elements/s
+BASELINE_ELEMS_PER_S = 1.41e7
+BASELINE_REFERENCE_STYLE = 1.16e6
+
+# Roofline of the round on one MI355X: the ARX cores are pure 32-bit VALU work that
+# no fusion removes -- XSalsa20 over every ciphertext byte twice (seal + open) and the
+# ChaCha20 share RNG -- at ~1000 lane-ops per 64-byte block against 256 CUs x 64
+# lanes x 2.4 GHz = 3.93e13 lane-ops/s.
+VALU_LANE_OPS_PER_S = 256 * 64 * 2.4e9
+ARX_OPS_PER_BLOCK = 1000.0
+
+
+def arx_floor_ms(P: int, D: int, n: int, m: int) -> float:
+    def vlen(v):
+        z, k = 2 * v, 1
+        while z >= 128:
+            z >>= 7
+            k += 1
+        return k
+    avg_len = sum(vlen(v) for v in range(m)) / m
+    salsa_blocks = 2 * (P * n * D * avg_len) / 64.0
+    draws_per_word = 3 if m ** 3 < 2 ** 32 else (2 if m <= 65536 else 1)
+    chacha_blocks = P * D * (n - 1) / (16.0 * draws_per_word)
+    return (salsa_blocks + chacha_blocks) * ARX_OPS_PER_BLOCK / VALU_LANE_OPS_PER_S * 1e3
 
 
 def parse():
@@ -58,20 +80,26 @@ def parse():
     ap.add_argument("--dim", type=int, default=1_000_000)
     ap.add_argument("--clerks", type=int, default=3)
     ap.add_argument("--modulus", type=int, default=433)
-    ap.add_argument("--check", action="store_true", help="verify the output every step")
+    ap.add_argument("--check", action="store_true",
+                    help="compare the output with the plain sum every step")
     ap.add_argument("--stages", action="store_true", help="print per-stage times (rank 0)")
-    ap.add_argument("--layout", default="owner", choices=["committee", "owner"],
-                    help="committee: boxes routed to the clerks' GPUs (protocol trust model); "
-                         "owner: each GPU hosts a slice of every clerk and opens its own "
-                         "participants' boxes (default)")
+    ap.add_argument("--layout", default="committee", choices=["committee", "owner"],
+                    help="N > 1. committee (default): sealed boxes routed to the clerks' GPUs, "
+                         "per-rank key custody, sealed results to rank 0. owner: non-private "
+                         "upper bound, each GPU opens its own participants' boxes")
     ap.add_argument("--waves", type=int, default=4,
                     help="committee layout: participant waves the exchange is pipelined over")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the distributed engine even on one rank (measures its overhead)")
-    ap.add_argument("--hw-queues", type=int, default=0,
-                    help="override GPU_MAX_HW_QUEUES (0 = leave the process default)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="process-group timeout in seconds: a rank that loses a peer exits non-zero")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="override GPU_MAX_HW_QUEUES for this process (A/B measurements); 0 = leave "
+                         "the environment's value, which is also what measured fastest")
+    ap.add_argument("--corrupt-step", type=int, default=-1,
+                    help="fault injection: flip a ciphertext bit in this timed step (the run must fail)")
     return ap.parse_args()
 
 
@@ -93,11 +121,14 @@ def main():
     torch.cuda.set_device(dev_index)
     dist_mode = world > 1 or args.force_dist
     if dist_mode:
+        timeout = datetime.timedelta(seconds=args.dist_timeout)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index),
+                                    timeout=timeout)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
 
+    from sda_amd.engine import reference_sum
     from sda_amd.models.schemes import Additive, AggregationSpec, NoMask
 
     spec = AggregationSpec(args.dim, args.modulus, Additive(args.clerks, args.modulus), NoMask(),
@@ -108,60 +139,90 @@ def main():
                             generator=gen)
 
     if not dist_mode:
-        from sda_amd.engine import DeviceAggregator, reference_sum
+        from sda_amd.engine import DeviceAggregator
 
         agg = DeviceAggregator(spec, time_stages=args.stages)
-
-        def step(check):
-            res = agg.run_round(secrets, check=check)
-            return res
-
-        expected = reference_sum(secrets, args.modulus) if args.check else None
+        engine, comm = agg, None
+        expected = reference_sum(secrets, args.modulus)
     else:
         from sda_amd.parallel.engine import DistributedAggregator
 
         agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", dev_index),
                                     time_stages=args.stages, layout=args.layout,
-                                    waves=args.waves, force_pipeline=args.force_dist)
+                                    waves=args.waves, force_pipeline=args.force_dist,
+                                    deadline_s=min(60.0, args.dist_timeout / 4))
+        engine, comm = agg.engine, agg.comm
+        # the global reference sum, reduced to rank 0
+        total = comm.reduce_sum(secrets.to(torch.int64).sum(0), dst=0)
+        expected = torch.remainder(total, args.modulus).to(torch.int32) if rank == 0 else None
 
-        def step(check):
-            return agg.run_round(secrets, check=check)
+    def verify(res, what):
+        if rank == 0 and not torch.equal(res.output, expected):
+            raise SystemExit(f"bench: {what}: aggregate does not match the reference sum")
 
-        expected = None
-        # the global reference sum, reduced to rank 0, validates the first warmup round
-        local = agg.comm.reduce_sum(secrets.to(torch.int64).sum(0), dst=0)
-        global_ref = torch.remainder(local, args.modulus).to(torch.int32) if rank == 0 else None
-
-    # warmup (also validates the result once)
+    # warmup: checked rounds (device error word + output)
     for i in range(args.warmup):
-        res = step(check=True)
-        if i == 0 and not dist_mode:
-            ref = reference_sum(secrets, args.modulus)
-            if not torch.equal(res.output, ref):
-                raise SystemExit("bench: device aggregation does not match the reference sum")
-        if i == 0 and dist_mode and rank == 0:
-            if not torch.equal(res.output, global_ref):
-                raise SystemExit("bench: distributed aggregation does not match the reference sum")
+        verify(agg.run_round(secrets, check=True), f"warmup round {i}")
     if dist_mode:
-        agg.comm.barrier()
+        comm.reset_audit()
+        comm.barrier()
     torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    err_total = torch.zeros(1, dtype=torch.int32, device="cuda")
+    res = None
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step(check=args.check)
-        if expected is not None and not torch.equal(res.output, expected):
-            raise SystemExit("bench: mismatch")
+    for i in range(args.steps):
+        if i == args.corrupt_step:
+            engine.corrupt_next_round()
+        res = agg.run_round(secrets, check=args.check)
+        err_total |= res.err  # device-side OR: read once, after the clock stops
+        if args.check:
+            verify(res, f"step {i}")
     torch.cuda.synchronize()
     if dist_mode:
-        agg.comm.barrier()
+        comm.barrier()
     elapsed = time.perf_counter() - t0
+    # integrity of the timed region: any MAC / varint / key / range failure in any
+    # step on any rank fails the run, and the last round's output must be right
+    e = int(err_total.item())
     if dist_mode:
-        elapsed = agg.comm.all_reduce_max(elapsed)
-    ms = elapsed / args.steps * 1e3
+        e = comm.all_reduce_or(e)
+        elapsed = comm.all_reduce_max(elapsed)
+    if e:
+        from sda_amd.engine import describe_error
+
+        raise SystemExit(f"bench: device error word 0x{e:x} in the timed steps ({describe_error(e)})")
+    if res is not None:
+        verify(res, "last timed round")
+    ms = elapsed / max(1, args.steps) * 1e3
     total_elems = P * world * args.dim
     value = total_elems / (ms / 1e3)
+    hbm_peak = torch.cuda.max_memory_allocated()
+    xgmi = None
+    if dist_mode:
+        hbm_peak = int(comm.all_reduce_max(float(hbm_peak)))
+        kinds = {}
+        for kind, direction, peer, _, nbytes in comm.audit:
+            if direction == "send" and peer != rank:
+                kinds[kind] = kinds.get(kind, 0) + nbytes
+        per_round = {k: v / max(1, args.steps) for k, v in kinds.items()}
+        xgmi = {"bytes_sent_per_rank_per_round": sum(per_round.values()),
+                "by_kind": per_round, "rank": rank}
     if rank == 0:
         if args.stages and getattr(res, "stage_ms", None):
             print(json.dumps({"stage_ms": res.stage_ms}), file=sys.stderr)
+        if not dist_mode:
+            parallelism = "single GPU"
+        elif args.layout == "committee":
+            parallelism = (f"dp{world} participants x committee-sharded clerks: all-to-all of "
+                           f"sealed boxes over xGMI (grouped RCCL send/recv, {args.waves} waves), "
+                           "per-rank key custody, sealed clerk results gathered on rank 0")
+            if world == 1:
+                parallelism += " [distributed engine on one rank: nothing crosses xGMI]"
+        else:
+            parallelism = (f"dp{world} owner (non-private upper bound): every GPU opens its own "
+                           "participants' boxes, plaintext clerk partials reduced to rank 0")
+        floor = arx_floor_ms(P, args.dim, args.clerks, args.modulus)
         line = {
             "metric": METRIC,
             "value": value,
@@ -172,9 +233,21 @@ def main():
             "ms_per_step": ms,
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": (value / BASELINE_ELEMS_PER_S) if BASELINE_ELEMS_PER_S else None,
+            "vs_baseline": value / BASELINE_ELEMS_PER_S,
+            "baseline": {"elements_per_s": BASELINE_ELEMS_PER_S,
+                         "what": "reference-equivalent CPU implementation measured here (8 threads, "
+                                 "buffered ChaCha20 RNG); the reference publishes no numbers",
+                         "vs_reference_style_single_thread": value / BASELINE_REFERENCE_STYLE},
+            "roofline_fraction": floor / ms,
+            "roofline": {"arx_valu_floor_ms_per_gpu": floor,
+                         "model": "XSalsa20 over the ciphertext twice + ChaCha20 share RNG at 1000 "
+                                  "lane-ops per 64 B block, 3.93e13 int32 lane-ops/s"},
             "dtype": "int32 (field elements mod 433; no floating point in this workload)",
             "data": "synthetic uniform random participant vectors in [0, 433)",
+            "hbm_high_water_bytes": hbm_peak,
+            "xgmi": xgmi,
+            "timed_steps_verified": "device error word of every timed step (OR over steps and "
+                                    "ranks) + last round's output vs the plain sum",
             "config": {
                 "model": f"SDA round: additive-{args.clerks} sharing, mod {args.modulus}, no mask, "
                          "libsodium sealed boxes (X25519+XSalsa20-Poly1305), zigzag varint",
@@ -183,12 +256,7 @@ def main():
                 "participants_per_gpu": P,
                 "dimension": args.dim,
                 "clerks": args.clerks,
-                "parallelism": (f"dp{world} participants x committee-sharded clerks: sealed "
-                                "boxes routed over xGMI (grouped RCCL send/recv), clerk partials "
-                                "reduced to rank 0" if args.layout == "committee" else
-                                f"dp{world} participants, every GPU hosting a slice of each clerk: clerk "
-                                "partials + mask partials reduced to rank 0 over RCCL")
-                               if world > 1 else "single GPU",
+                "parallelism": parallelism,
             },
         }
         print(json.dumps(line), flush=True)

@@ -28,7 +28,7 @@ import torch
 from ._native import native
 from .models.schemes import Additive, AggregationSpec, ChaChaMask, FullMask, PackedShamir
 from .ops import gpu as G
-from .ops.sealed import (Arena, open_, open_data, open_setup, open_sum, seal, seal_data,
+from .ops.sealed import (Arena, KeySet, open_, open_data, open_setup, open_sum, seal, seal_data,
                          seal_setup)
 from .utils.trace import tracing_enabled
 
@@ -44,18 +44,71 @@ class AggregationError(RuntimeError):
     pass
 
 
+_SIDE_STREAMS: dict = {}
+
+
+def concurrent_stream(device, tries: int = 12, spin_us: int = 250) -> "torch.cuda.Stream":
+    """A stream whose kernels really run beside the current stream's.
+
+    HIP multiplexes a process's streams onto few hardware queues (4 by default),
+    and two streams on one queue serialise -- which of them share a queue
+    depends on how many streams the process (and RCCL) created before. The
+    side stream carries latency-bound X25519 ladders that must overlap the
+    main stream's bulk kernels, so candidates are probed: the main stream runs
+    a bounded 250 us wait (a gate the host never posts), the candidate a no-op;
+    a candidate that finishes while the wait is still running sits on another
+    queue. Falls back to the last candidate (correct, only slower)."""
+    dev = torch.device(device)
+    main = torch.cuda.current_stream(dev)
+    key = (dev.index, main.cuda_stream)
+    if key in _SIDE_STREAMS:
+        return _SIDE_STREAMS[key]
+    gate = torch.zeros(1, dtype=torch.int32, device=dev)
+    cand = None
+    with torch.cuda.device(dev):
+        for _ in range(tries):
+            cand = torch.cuda.Stream(device=dev)
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            torch.cuda.synchronize(dev)
+            e0.record(main)
+            G.gate_wait((gate, 1), timeout_us=spin_us)  # main: never posted, ends at the limit
+            with torch.cuda.stream(cand):
+                G.gate_wait((gate, 0), timeout_us=1)    # candidate: returns at once
+                e1.record(cand)
+            e2.record(main)
+            torch.cuda.synchronize(dev)
+            if e0.elapsed_time(e1) < 0.5 * e0.elapsed_time(e2):
+                break
+    _SIDE_STREAMS[key] = cand
+    return cand
+
+
 def _words(b: bytes) -> list[int]:
     return [int.from_bytes(b[4 * i:4 * i + 4], "little", signed=True) for i in range(len(b) // 4)]
 
 
 @dataclass
 class KeyTable:
-    """X25519 keypairs: index 0..n-1 = clerks, index n = recipient."""
+    """X25519 keypairs: index 0..n-1 = clerks, index n = recipient.
+
+    A process that plays only some of the parties holds only their secret
+    keys: `sk_bytes[i]` is None (and row i of `sks` zero) for the others."""
 
     pks: torch.Tensor  # int32 [K][8]
     sks: torch.Tensor  # int32 [K][8]
     pk_bytes: list = field(default_factory=list)
     sk_bytes: list = field(default_factory=list)
+
+    @classmethod
+    def from_bytes(cls, pk: list, sk: list, device) -> "KeyTable":
+        zero = bytes(32)
+        pks = torch.tensor([_words(p) for p in pk], dtype=torch.int32, device=device)
+        sks = torch.tensor([_words(s if s is not None else zero) for s in sk], dtype=torch.int32,
+                           device=device)
+        return cls(pks, sks, list(pk), list(sk))
+
+    def holds(self, i: int) -> bool:
+        return self.sk_bytes[i] is not None
 
     @classmethod
     def generate(cls, count: int, device) -> "KeyTable":
@@ -73,6 +126,10 @@ class RoundResult:
     output: torch.Tensor          # int32 [D], canonical in [0, m)
     clerks_used: list
     stage_ms: dict
+    # the round's device error word (int32 [1]; see describe_error). Already
+    # read and raised on when the round ran with check=True; callers that time
+    # unchecked rounds OR these together and read the result once.
+    err: Optional[torch.Tensor] = None
 
 
 class DeviceAggregator:
@@ -190,7 +247,7 @@ class DeviceAggregator:
         if getattr(self, "_side", None) is None:
             # default priority, like every stream of the process: its kernels are
             # latency-bound X25519 ladders that raise their own wave priority
-            self._side = torch.cuda.Stream(device=self.device)
+            self._side = concurrent_stream(self.device)
         return self._side
 
     def _live(self, clerks):
@@ -202,42 +259,40 @@ class DeviceAggregator:
             raise AggregationError("Not enough shares to reconstruct")
         return live
 
+    def corrupt_next_round(self) -> None:
+        """Fault injection: flip one ciphertext bit of the next round's first
+        sealed box in transit (the clerk's MAC check must then fail the round)."""
+        self._corrupt = True
+
+    def _inject_corruption(self, arena: Arena) -> None:
+        if getattr(self, "_corrupt", False):
+            self._corrupt = False
+            arena.ct[G.SEAL_OVERHEAD + 5] ^= 1
+
     def new_error_word(self) -> torch.Tensor:
         return torch.zeros(1, dtype=torch.int32, device=self.device)
 
     def run_round(self, secrets: torch.Tensor, clerks: Sequence[int] | None = None,
-                  check: bool = True, reducer=None, owner_base: int = 0,
-                  router=None, router_for=None, waves: int = 1) -> RoundResult:
+                  check: bool = True, reducer=None, owner_base: int = 0) -> RoundResult:
         """One full round for participant vectors `secrets` [P][D] (int32, on device).
 
         = :meth:`participate_and_clerk` (+ `reducer`) + :meth:`reveal`.
 
-        `reducer(partials) -> reduced | None` (multi-GPU): called with the
-        per-clerk column sums over this device's participants -- int64
-        [len(live) (+1 with a mask)][max(B, D)] -- before the recipient stage;
-        it returns the sums over all devices on the root and None elsewhere
-        (which then skips the recipient stage and returns ``output=None``).
-        `owner_base` offsets the participants' RNG stream ids.
-        `router.exchange(arena) -> inbox` (multi-GPU committee layout): moves
-        the sealed clerk boxes to the ranks that play the clerks; the clerk
-        stage then opens the inbox (same [n][P] clerk-major shape). With
-        `router_for(P_wave)` and `waves > 1` the exchange is pipelined behind
-        the next wave's compute (:meth:`participate_and_clerk_pipelined`).
+        `reducer(partials) -> reduced | None` (the multi-GPU ``owner`` layout,
+        a non-private upper bound): called with the per-clerk column sums over
+        this device's participants -- int64 [len(live) (+1 with a mask)][max(B,
+        D)] -- before the recipient stage; it returns the sums over all
+        devices on the root and None elsewhere (which then skips the recipient
+        stage and returns ``output=None``). `owner_base` offsets the
+        participants' RNG stream ids. The protocol-faithful multi-GPU round is
+        :class:`sda_amd.parallel.DistributedAggregator`'s ``committee`` layout.
         """
         live = self._live(clerks)
         err = self.new_error_word()
         marks: list = []
         self._mark(marks, "start")
-        if router_for is not None and waves > 1:
-            self._mark(marks, "participate")
-            combined, mask_sum = self.participate_and_clerk_pipelined(
-                secrets, live, err, router_for, waves, owner_base=owner_base, marks=marks)
-        else:
-            if router is None and router_for is not None:
-                router = router_for(secrets.shape[0])
-            combined, mask_sum = self.participate_and_clerk(secrets, live, err,
-                                                            owner_base=owner_base, router=router,
-                                                            marks=marks)
+        combined, mask_sum = self.participate_and_clerk(secrets, live, err, owner_base=owner_base,
+                                                        marks=marks)
         # the recipient's key agreement queues on the side stream BEHIND the
         # participants' and clerks' (needed last; ahead of them it delayed the
         # first encrypt by the length of an X25519 ladder)
@@ -250,7 +305,7 @@ class DeviceAggregator:
         return self._finish(err, marks, check, RoundResult(out, live, {}))
 
     def participate_and_clerk(self, secrets: torch.Tensor, live, err, owner_base: int = 0,
-                              router=None, marks=None):
+                              marks=None):
         """Participants mask + share + seal; clerks open + combine.
 
         Returns (combined [len(live)][B] int32 in [0, m), mask_sum [D] int32 or
@@ -264,144 +319,13 @@ class DeviceAggregator:
         the main stream waits on events only where it consumes derived keys.
         """
         marks = [] if marks is None else marks
-        st = self._participate(secrets, live, err, owner_base, local_clerks=router is None)
+        st = self._participate(secrets, live, err, owner_base)
         self._mark(marks, "participate")
-        if router is not None:
-            # snapshot transpose over xGMI: boxes travel to the clerks' ranks
-            st["inbox"] = router.exchange(st.pop("clerk_arena"))
-            self._mark(marks, "exchange")
         out = self._clerk(st, live, err)
         self._mark(marks, "clerk")
         return out
 
-    def participate_and_clerk_pipelined(self, secrets: torch.Tensor, live, err, router_for,
-                                        waves: int, owner_base: int = 0, marks=None):
-        """Committee layout with the exchange hidden behind compute.
-
-        X25519 setup is latency-bound (one ladder per thread, ~1.7 ms however
-        few messages), so key agreement is done once per round, not per wave:
-        one seal setup for every box of the round (a wave-blocked clerk-major
-        arena: wave w's n * P_w slots are contiguous), then the 32-byte
-        ephemeral-key headers travel ahead of the data over the same routing
-        plan so the clerks derive all their open keys on the side stream while
-        the waves are being sealed. Per wave: mask + share + seal, grouped
-        send/recv on the communicator stream (overlapping the next wave's
-        compute), open + combine once it has landed.
-        """
-        spec, n, m = self.spec, self.n, self.m
-        marks = [] if marks is None else marks
-        if secrets.dim() != 2 or secrets.shape[1] != spec.dimension:
-            raise ValueError("secrets must be [P][dimension]")
-        secrets = secrets.contiguous()
-        P, D = secrets.shape
-        B, dev = spec.batches, self.device
-        bounds = [(P * w // waves, P * (w + 1) // waves) for w in range(waves)]
-        bounds = [(lo, hi) for lo, hi in bounds if hi > lo]
-        rng_key = native().crypto.random_bytes(32)
-        self._round += 1
-        main = torch.cuda.current_stream(dev)
-        side = self._side_stream()
-        pks, sks = self.keys.pks, self.keys.sks
-
-        arena = Arena.empty(n * P, B, m, dev)
-        inbox = Arena(arena.M, arena.L, arena.modulus, arena.stride, arena.K,
-                      torch.empty_like(arena.ct), torch.empty_like(arena.pt_len))
-        kidx = torch.cat([self._kidx_clerk(hi - lo) for lo, hi in bounds])
-        mask_arena = None
-        if isinstance(spec.masking, FullMask):
-            mask_arena = Arena.empty(P, D, m, dev)
-        elif isinstance(spec.masking, ChaChaMask):
-            mask_arena = Arena.empty(P, spec.masking.seed_words, 0, dev)
-        kidx_rcpt = torch.full((P,), n, dtype=torch.int32, device=dev)
-
-        gate = self._gate_token()
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            ks = seal_setup(arena, kidx, pks, rng_key, 0, err, gate=gate).with_powers()
-            ks_mask = ko_mask = None
-            if mask_arena is not None:
-                ks_mask = seal_setup(mask_arena, kidx_rcpt, pks, rng_key, n * P, err).with_powers()
-                ko_mask = open_setup(mask_arena, kidx_rcpt, sks, pks, err)
-            ev_seal = torch.cuda.Event()
-            ev_seal.record(side)
-        # caching-allocator stream bookkeeping: side-allocated keys are consumed on
-        # main, main-allocated buffers are touched on side
-        for t in (ks, ks_mask, ko_mask):
-            if t is not None:
-                t.record_stream(main)
-        for t in (arena.ct, kidx, kidx_rcpt) + ((mask_arena.ct,) if mask_arena is not None else ()):
-            t.record_stream(side)
-
-        def start_headers():
-            """Ephemeral-key headers ahead of the data (tiny), then the clerks'
-            open keys on the side stream; returns the event to wait on."""
-            hdr = torch.empty(arena.M, 32, dtype=torch.uint8, device=dev)
-            hdr_in = torch.empty_like(hdr)
-            main.wait_event(ev_seal)
-            hdr.copy_(arena.ct.view(arena.M, arena.stride)[:, :32])
-            sends, recvs = [], []
-            for lo, hi in bounds:
-                s_, r_, _ = router_for(hi - lo).row_ops(hdr, hdr_in, base=n * lo)
-                sends += s_
-                recvs += r_
-            h_hdr = self.comm_exchange(router_for, sends, recvs)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                h_hdr.wait()
-                inbox.ct.view(inbox.M, inbox.stride)[:, :32].copy_(hdr_in)
-                keys = open_setup(inbox, kidx, sks, pks, err)
-                ev = torch.cuda.Event()
-                ev.record(side)
-            keys.record_stream(main)
-            for t in (hdr, hdr_in, inbox.ct, inbox.pt_len):
-                t.record_stream(side)
-            self._mark(marks, "keys")
-            return keys, ev
-
-        acc = macc = None
-        pending = None
-
-        def finish(st):
-            nonlocal acc, macc
-            lo, hi, handle = st
-            Pw = hi - lo
-            handle.wait()
-            main.wait_event(ev_open)
-            comb = self._open_combine(inbox.slice(n * lo, n * Pw), ko.slice(n * lo, n * Pw),
-                                      live, Pw, err)
-            acc = comb if acc is None else acc + comb
-            if mask_arena is not None:
-                msum = self._open_masks(mask_arena.slice(lo, Pw), ko_mask.slice(lo, Pw), err)
-                macc = msum if macc is None else macc + msum
-
-        ko = ev_open = None
-        G.gate_wait(gate)
-        for lo, hi in bounds:
-            Pw = hi - lo
-            shares, cnt, mvals, mcnt = self._share(secrets[lo:hi], rng_key, owner_base + lo, err)
-            if ko is None:  # the first wave's shares overlap the whole-round seal setup
-                ko, ev_open = start_headers()
-            box = arena.slice(n * lo, n * Pw)
-            seal_data(box, ks.slice(n * lo, n * Pw), shares.view(n * Pw, B), err, cnt)
-            del shares
-            if mask_arena is not None:
-                seal_data(mask_arena.slice(lo, Pw), ks_mask.slice(lo, Pw), mvals, err, mcnt)
-            _, handle = router_for(Pw).exchange_async(box, inbox=inbox.slice(n * lo, n * Pw))
-            if pending is not None:
-                finish(pending)
-            pending = (lo, hi, handle)
-        finish(pending)
-        self._mark(marks, "clerk")
-        multi = len(bounds) > 1
-        return (torch.remainder(acc, m) if multi else acc,
-                torch.remainder(macc, m) if (macc is not None and multi) else macc)
-
-    @staticmethod
-    def comm_exchange(router_for, sends, recvs):
-        """Grouped P2P through the routers' communicator (any wave size's router)."""
-        return router_for(None).comm.exchange_async(sends, recvs) if sends or recvs else _NoWait()
-
-    def _participate(self, secrets, live, err, owner_base, local_clerks: bool):
+    def _participate(self, secrets, live, err, owner_base):
         """Mask + share + seal one batch of participants; returns the state the
         clerk half needs (arenas and derived keys)."""
         spec, n, m = self.spec, self.n, self.m
@@ -443,8 +367,7 @@ class DeviceAggregator:
 
         def open_keys():
             with torch.cuda.stream(side):
-                ko_clerk = self._open_keys(clerk_arena, kidx_clerk, live, P, err) \
-                    if local_clerks else None
+                ko_clerk = self._open_keys(clerk_arena, kidx_clerk, live, P, err)
                 ko_mask = (open_setup(mask_arena, kidx_rcpt_p, self.keys.sks, pks, err)
                            if mask_arena is not None else None)
                 ev_openkeys = torch.cuda.Event()
@@ -460,21 +383,17 @@ class DeviceAggregator:
         if _OPEN_AFTER_SHARE:
             side.wait_stream(main)
             ko_clerk, ko_mask, ev_openkeys = open_keys()
-        for t in [ks_clerk, ks_mask, ko_mask] + (ko_clerk or []):
+        for t in [ks_clerk, ks_mask, ko_mask] + ko_clerk:
             if t is not None:
                 t.record_stream(main)
         main.wait_event(ev_sealkeys)
         seal_data(clerk_arena, ks_clerk, shares.view(n * P, B), err, cnt)
         del shares
+        self._inject_corruption(clerk_arena)
         if mask_arena is not None:
             seal_data(mask_arena, ks_mask, mask_vals, err, mask_cnt)
-        st = {"P": P, "kidx": kidx_clerk, "ev_openkeys": ev_openkeys, "mask_arena": mask_arena,
-              "ko_mask": ko_mask}
-        if local_clerks:
-            st["inbox"], st["ko_clerk"] = clerk_arena, ko_clerk
-        else:
-            st["clerk_arena"] = clerk_arena
-        return st
+        return {"P": P, "kidx": kidx_clerk, "ev_openkeys": ev_openkeys, "mask_arena": mask_arena,
+                "ko_mask": ko_mask, "inbox": clerk_arena, "ko_clerk": ko_clerk}
 
     def _clerk(self, st, live, err):
         """Open + combine an inbox (the local arena or the routed one)."""
@@ -482,7 +401,7 @@ class DeviceAggregator:
         main = torch.cuda.current_stream(self.device)
         main.wait_event(st["ev_openkeys"])
         inbox = st.pop("inbox")
-        ko_clerk = st.get("ko_clerk") or self._open_keys(inbox, st["kidx"], live, P, err)
+        ko_clerk = st["ko_clerk"]
         combined = self._open_combine(inbox, ko_clerk, live, P, err)
         del inbox
         # recipient's share of the mask work is data-parallel too: open these
@@ -575,13 +494,42 @@ class DeviceAggregator:
             keys = self.prepare_reveal(live, err)
         res_arena, ks_res, ko_res, ev = keys
         torch.cuda.current_stream(dev).wait_event(ev)
+        self.seal_results(res_arena, ks_res, combined, err)
+        out = self.open_results(res_arena, ko_res, live, err, mask_sum)
+        if marks is not None:
+            self._mark(marks, "reveal")
+        return out
+
+    def seal_results(self, res_arena: Arena, ks_res: KeySet, combined: torch.Tensor, err) -> Arena:
+        """Clerk side of the result path (clerk.rs:99-100): seal the combined
+        shares -- one row per clerk -- for the recipient."""
         res_vals = combined if self.vdtype == torch.int32 else combined.to(self.vdtype)
-        seal_data(res_arena, ks_res, res_vals, err)
+        return seal_data(res_arena, ks_res, res_vals, err)
+
+    def open_results(self, res_arena: Arena, ko_res: KeySet, live, err, mask_sum=None,
+                     rows: Sequence[int] | None = None) -> torch.Tensor:
+        """Recipient side (receive.rs:127-152): open the clerks' sealed results,
+        reconstruct (sum / Lagrange over the clerks `live`) and unmask.
+
+        `res_arena` row i holds clerk live[i]'s result, or -- with `rows` --
+        row rows[i] does (results that never arrived leave their rows unused)."""
+        spec, m = self.spec, self.m
+        D, dev = spec.dimension, self.device
         masked = torch.empty(D, dtype=torch.int32, device=dev)
+        if rows is not None and list(rows) == list(range(res_arena.M)):
+            rows = None
         if self._pss is None:  # additive: the reconstruction is the sum of the n results
+            if rows is not None or len(live) != self.n:
+                raise AggregationError("additive sharing needs every clerk's result")
             open_sum(res_arena, ko_res, err, rows=1, out=masked)
         else:
-            ys = open_data(res_arena, ko_res, err, out_dtype=torch.int32)
+            if len(live) < spec.sharing.reconstruction_threshold():
+                raise AggregationError("Not enough shares to reconstruct")
+            if rows is None:
+                ys = open_data(res_arena, ko_res, err, out_dtype=torch.int32)
+            else:
+                ys = torch.cat([open_data(res_arena.slice(r, 1), ko_res.slice(r, 1), err,
+                                          out_dtype=torch.int32) for r in rows])
             if self._pss_mfma:
                 lag_limbs, kp = self._lagrange_limbs(live)
                 G.modgemm_i8(lag_limbs, G.limbs_t(ys, kp, self._limbs), m, masked, ldc_z=0,
@@ -593,8 +541,6 @@ class DeviceAggregator:
         if mask_sum is not None:
             out = torch.empty(D, dtype=torch.int32, device=dev)
             G.sub_mod(masked, mask_sum, m, out)
-        if marks is not None:
-            self._mark(marks, "reveal")
         return out
 
     def _kidx_clerk(self, P: int) -> torch.Tensor:
@@ -614,6 +560,7 @@ class DeviceAggregator:
                 for c in live]
 
     def _finish(self, err, marks, check, result: RoundResult) -> RoundResult:
+        result.err = err
         if check or self.time_stages:
             e = int(err.item())
             if e:
@@ -642,11 +589,6 @@ class DeviceAggregator:
             cache[key] = torch.tensor(self._pss.lagrange_matrix(list(live)), dtype=torch.int64).to(
                 torch.int32).to(self.device)
         return cache[key]
-
-
-class _NoWait:
-    def wait(self):
-        pass
 
 
 def describe_error(e: int) -> str:

@@ -1,6 +1,6 @@
 """Host (CPU) aggregation engine: the reference dataflow on the C++ client engines.
 
-Same round semantics and `run_round` interface as the device engine
+Same round semantics as the device engine
 (:class:`sda_amd.engine.DeviceAggregator`), but every step is the per-participant
 client code path of the reference (client/src/participate.rs:37-113,
 clerk.rs:63-107, receive.rs:80-157) executed by the C++ core: OS-RNG masks and
@@ -8,13 +8,18 @@ shares, zigzag varints, one sealed box per (participant, clerk). It is the
 correctness oracle for the device engine, the CPU backend of
 :class:`sda_amd.parallel.DistributedAggregator` (gloo tests), and the
 reference-equivalent baseline.
+
+The round is exposed both whole (:meth:`HostAggregator.run_round`) and as the
+role steps the distributed engine composes (``participate`` -> ``clerk_combine``
+-> ``seal_result`` -> ``reveal``); a step that needs a secret key this process
+does not hold raises.
 """
 from __future__ import annotations
 
 import json
 import time
 from dataclasses import dataclass, field
-from typing import Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -25,7 +30,8 @@ from .models.schemes import AggregationSpec, PackedShamir
 
 @dataclass
 class HostKeys:
-    """X25519 keypairs as raw bytes: index 0..n-1 = clerks, index n = recipient."""
+    """X25519 keypairs as raw bytes: index 0..n-1 = clerks, index n = recipient.
+    ``sks[i]`` is None where this process does not hold the secret key."""
 
     pks: list
     sks: list
@@ -39,6 +45,8 @@ class HostKeys:
         return json.dumps(C.sodium(self.pks[i]))
 
     def keypair(self, i: int) -> str:
+        if self.sks[i] is None:
+            raise PermissionError(f"this process does not hold the secret key of party {i}")
         return json.dumps({"ek": C.sodium(self.pks[i]), "dk": C.sodium(self.sks[i])})
 
 
@@ -59,76 +67,107 @@ class HostAggregator:
         self._share = json.dumps(spec.sharing.to_wire())
         self._c = native().control
 
-    def run_round(self, secrets, clerks: Sequence[int] | None = None, check: bool = True,
-                  reducer=None, owner_base: int = 0, router=None) -> HostRoundResult:
-        spec, n, m, c = self.spec, self.n, self.m, self._c
+    # ---- role steps -----------------------------------------------------------
+    def live(self, clerks: Sequence[int] | None) -> List[int]:
+        live = list(range(self.n)) if clerks is None else sorted(set(int(x) for x in clerks))
+        if len(live) < self.spec.sharing.reconstruction_threshold():
+            raise C.errors.SdaError("Not enough shares to reconstruct")
+        return live
+
+    def participate(self, secrets) -> Tuple[list, Optional[list]]:
+        """participate.rs:37-113 for every row of `secrets`: (boxes [P][n] sealed
+        for the clerks, mask boxes [P] sealed for the recipient or None)."""
+        spec, n, c = self.spec, self.n, self._c
         secrets = np.asarray(secrets, dtype=np.int64)
         if secrets.ndim != 2 or secrets.shape[1] != spec.dimension:
             raise ValueError("secrets must be [P][dimension]")
-        P, D = secrets.shape
-        B = spec.batches
-        live = list(range(n)) if clerks is None else sorted(set(int(x) for x in clerks))
-        if len(live) < spec.sharing.reconstruction_threshold():
-            raise C.errors.SdaError("Not enough shares to reconstruct")
-        t = {"start": time.perf_counter()}
-
-        # participants (participate.rs:37-113)
-        boxes = []        # [P][n] sealed share vectors
-        mask_boxes = []   # [P] sealed masks for the recipient
-        for p in range(P):
+        boxes, mask_boxes = [], []
+        for p in range(secrets.shape[0]):
             mask, masked = c.mask_secrets(self._mask, secrets[p].tolist())
             shares = c.generate_shares(self._share, masked)
             boxes.append([c.encrypt_shares(self.keys.ek(j), shares[j]) for j in range(n)])
             if spec.masking.has_mask():
                 mask_boxes.append(c.encrypt_shares(self.keys.ek(n), mask))
-        t["participate"] = time.perf_counter()
+        return boxes, (mask_boxes if spec.masking.has_mask() else None)
 
-        # clerks: open this device's participants' boxes and combine (clerk.rs:63-107)
-        # snapshot transpose: P x n -> n x P (locally, or routed to the clerks' ranks)
-        inbox = (router.exchange_host(boxes) if router is not None
-                 else [[boxes[p][j] for p in range(P)] for j in range(n)])
-        combined = np.zeros((len(live), B), dtype=np.int64)
-        for i, j in enumerate(live):
-            kp = self.keys.keypair(j)
-            acc = np.zeros(B, dtype=np.int64)
-            for box in inbox[j]:
-                acc += np.asarray(c.decrypt_shares(kp, box), dtype=np.int64)
-            combined[i] = np.remainder(acc, m)
-        mask_sum = None
-        if spec.masking.has_mask():
-            rk = self.keys.keypair(n)
-            masks = [c.decrypt_shares(rk, mb) for mb in mask_boxes]
-            mask_sum = np.remainder(np.asarray(c.combine_masks(self._mask, masks), dtype=np.int64), m)
-        t["clerk"] = time.perf_counter()
+    def clerk_combine(self, clerk: int, boxes: Sequence[str]) -> np.ndarray:
+        """clerk.rs:79-86: open the boxes sealed for `clerk` and sum mod m."""
+        kp = self.keys.keypair(clerk)
+        acc = np.zeros(self.spec.batches, dtype=np.int64)
+        for box in boxes:
+            acc += np.asarray(self._c.decrypt_shares(kp, box), dtype=np.int64)
+        return np.remainder(acc, self.m)
 
-        if reducer is not None:
-            rows = len(live) + (1 if mask_sum is not None else 0)
-            partials = np.zeros((rows, max(B, D)), dtype=np.int64)
-            partials[:len(live), :B] = combined
-            if mask_sum is not None:
-                partials[len(live), :D] = mask_sum
-            reduced = reducer(partials)
-            t["reduce"] = time.perf_counter()
-            if reduced is None:
-                return HostRoundResult(None, live, _ms(t))
-            reduced = np.remainder(np.asarray(reduced, dtype=np.int64), m)
-            combined = reduced[:len(live), :B]
-            if mask_sum is not None:
-                mask_sum = reduced[len(live), :D]
+    def seal_result(self, combined: np.ndarray) -> str:
+        """clerk.rs:99-100: the clerk's combined shares sealed for the recipient."""
+        return self._c.encrypt_shares(self.keys.ek(self.n), np.asarray(combined).tolist())
 
-        # clerks seal results for the recipient; recipient reconstructs + unmasks
-        rkp = self.keys.keypair(n)
-        indexed = []
-        for i, j in enumerate(live):
-            box = c.encrypt_shares(self.keys.ek(n), combined[i].tolist())
-            indexed.append((j, c.decrypt_shares(rkp, box)))
+    def reveal(self, results: Sequence[Tuple[int, str]], mask_boxes: Optional[Sequence[str]]):
+        """receive.rs:102-152: open the clerks' results (committee index, box),
+        reconstruct, open + combine the masks, unmask."""
+        spec, c, m, D = self.spec, self._c, self.m, self.spec.dimension
+        rkp = self.keys.keypair(self.n)
+        if len(results) < spec.sharing.reconstruction_threshold():
+            raise C.errors.SdaError("Not enough shares to reconstruct")
+        indexed = [(j, c.decrypt_shares(rkp, box)) for j, box in results]
         if isinstance(spec.sharing, PackedShamir):
             out = c.reconstruct_secrets(self._share, D, indexed)
         else:
             out = np.remainder(np.sum([np.asarray(v, dtype=np.int64) for _, v in indexed], 0), m)
             out = out.tolist()
-        if mask_sum is not None:
+        if spec.masking.has_mask():
+            masks = [c.decrypt_shares(rkp, mb) for mb in mask_boxes]
+            mask_sum = np.remainder(np.asarray(c.combine_masks(self._mask, masks), dtype=np.int64), m)
             out = c.unmask(self._mask, mask_sum.tolist(), out)
+        return np.remainder(np.asarray(out, dtype=np.int64), m)
+
+    # ---- the whole round in one process ------------------------------------------
+    def run_round(self, secrets, clerks: Sequence[int] | None = None, check: bool = True,
+                  reducer=None, owner_base: int = 0) -> HostRoundResult:
+        """One round. `reducer(partials) -> reduced | None` (the ``owner``
+        multi-process layout): sums the per-clerk partial sums and the mask
+        partial over processes onto the root."""
+        spec, n, m = self.spec, self.n, self.m
+        live = self.live(clerks)
+        t = {"start": time.perf_counter()}
+        boxes, mask_boxes = self.participate(secrets)
+        P, D, B = len(boxes), spec.dimension, spec.batches
+        t["participate"] = time.perf_counter()
+        # snapshot transpose (snapshot.rs:11-27): P x n -> n x P
+        combined = np.stack([self.clerk_combine(j, [boxes[p][j] for p in range(P)]) for j in live])
+        t["clerk"] = time.perf_counter()
+        if reducer is None:
+            results = [(j, self.seal_result(combined[i])) for i, j in enumerate(live)]
+            out = self.reveal(results, mask_boxes)
+            t["reveal"] = time.perf_counter()
+            return HostRoundResult(out, live, _ms(t))
+
+        # owner layout: plaintext partials are summed across processes
+        c = self._c
+        mask_sum = None
+        if mask_boxes is not None:
+            rk = self.keys.keypair(n)
+            masks = [c.decrypt_shares(rk, mb) for mb in mask_boxes]
+            mask_sum = np.remainder(np.asarray(c.combine_masks(self._mask, masks), dtype=np.int64), m)
+        rows = len(live) + (1 if mask_sum is not None else 0)
+        partials = np.zeros((rows, max(B, D)), dtype=np.int64)
+        partials[:len(live), :B] = combined
+        if mask_sum is not None:
+            partials[len(live), :D] = mask_sum
+        reduced = reducer(partials)
+        t["reduce"] = time.perf_counter()
+        if reduced is None:
+            return HostRoundResult(None, live, _ms(t))
+        reduced = np.remainder(np.asarray(reduced, dtype=np.int64), m)
+        results = [(j, self.seal_result(reduced[i, :B])) for i, j in enumerate(live)]
+        rkp = self.keys.keypair(n)
+        indexed = [(j, c.decrypt_shares(rkp, box)) for j, box in results]
+        if isinstance(spec.sharing, PackedShamir):
+            out = c.reconstruct_secrets(self._share, D, indexed)
+        else:
+            out = np.remainder(np.sum([np.asarray(v, dtype=np.int64) for _, v in indexed], 0), m).tolist()
+        if mask_sum is not None:
+            out = c.unmask(self._mask, reduced[len(live), :D].tolist(), out)
         t["reveal"] = time.perf_counter()
         return HostRoundResult(np.remainder(np.asarray(out, dtype=np.int64), m), live, _ms(t))
 

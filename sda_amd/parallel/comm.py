@@ -1,10 +1,29 @@
-"""Collectives for the aggregation engines.
+"""Collectives, point-to-point transfers and the liveness rendezvous of the
+distributed engines.
 
 With the ``nccl`` backend (RCCL on ROCm, over xGMI) tensors stay on the GPU.
 With ``gloo`` (CPU tests, or several ranks sharing one GPU) device tensors are
-staged through host memory, so the same engine code runs on both.
+staged through host memory with synchronous copies, so the same engine code
+runs on both.
+
+Every payload that leaves a rank is recorded in ``Comm.audit`` as
+``(kind, direction, peer, clerk, nbytes)``: tests assert from it that plaintext
+partial sums only ever travel between hosts of the same clerk, and the bench
+reports the bytes a rank puts on xGMI per round.
+
+The rendezvous (``arrive`` / ``decide`` / ``decision``) is the reference's
+result polling (client/src/receive.rs:86-96, server/src/server.rs:104-129: a
+snapshot is ready once enough clerking results were posted) on the process
+group's key-value store: a clerk that has reached the result stage posts a
+flag, the recipient waits for the flags up to a deadline and publishes which
+clerks it will read, and only those send. A clerk whose process died never
+posts, so no rank ever waits on a transfer from a dead peer.
 """
 from __future__ import annotations
+
+import time
+from datetime import timedelta
+from typing import Iterable, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -12,7 +31,7 @@ import torch.distributed as dist
 
 
 class Comm:
-    def __init__(self, group=None):
+    def __init__(self, group=None, deadline_s: float = 60.0):
         if not dist.is_initialized():
             raise RuntimeError("torch.distributed is not initialised")
         self.group = group
@@ -20,13 +39,28 @@ class Comm:
         self.world = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
         self.device_native = self.backend == "nccl"
+        self.deadline_s = float(deadline_s)
+        self.audit: List[tuple] = []
+        self._store = None
+
+    # -- accounting -------------------------------------------------------------
+    def note(self, kind: str, direction: str, peer: int, clerk: int, nbytes: int):
+        self.audit.append((kind, direction, peer, clerk, int(nbytes)))
+
+    def bytes_sent(self, kinds: Optional[Iterable[str]] = None) -> int:
+        ks = None if kinds is None else set(kinds)
+        return sum(n for k, d, p, _, n in self.audit
+                   if d == "send" and p != self.rank and (ks is None or k in ks))
+
+    def reset_audit(self):
+        self.audit = []
 
     # -- staging helpers ------------------------------------------------------
     def _to_wire(self, t):
         if isinstance(t, np.ndarray):
             return torch.from_numpy(np.ascontiguousarray(t)), "numpy", None
         if t.is_cuda and not self.device_native:
-            return t.cpu(), "cuda", t.device
+            return t.cpu(), "cuda", t.device  # synchronous copy: gloo only sees host memory
         return t, "torch", None
 
     @staticmethod
@@ -36,6 +70,9 @@ class Comm:
         if kind == "cuda":
             return w.to(device)
         return w
+
+    def _wire_device(self):
+        return torch.device("cuda", torch.cuda.current_device()) if self.device_native else "cpu"
 
     # -- collectives ------------------------------------------------------------
     def barrier(self):
@@ -49,6 +86,15 @@ class Comm:
         dist.broadcast(w, src=src, group=self.group)
         return self._from_wire(w, kind, dev)
 
+    def broadcast_bytes(self, data: Optional[bytes], nbytes: int, src: int = 0) -> bytes:
+        """Public data (e.g. a public key) from `src` to everyone."""
+        buf = torch.zeros(nbytes, dtype=torch.uint8)
+        if self.rank == src:
+            buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).clone()
+        buf = buf.to(self._wire_device())
+        dist.broadcast(buf, src=src, group=self.group)
+        return bytes(buf.cpu().numpy().tobytes())
+
     def reduce_sum(self, t, dst: int = 0):
         """Sum over ranks; the result on `dst`, None elsewhere."""
         w, kind, dev = self._to_wire(t)
@@ -57,57 +103,51 @@ class Comm:
         return self._from_wire(w, kind, dev) if self.rank == dst else None
 
     def all_reduce_max(self, value: float) -> float:
-        dev = torch.device("cuda", torch.cuda.current_device()) if self.device_native else "cpu"
-        t = torch.tensor([value], dtype=torch.float64, device=dev)
+        t = torch.tensor([value], dtype=torch.float64, device=self._wire_device())
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return float(t.item())
 
-    def all_to_all_equal(self, out: torch.Tensor, inp: torch.Tensor):
-        """Equal-split all-to-all of a flat buffer (rank r gets block r of every rank)."""
-        w_in, kind, dev = self._to_wire(inp)
-        if kind == "cuda":
-            w_out = torch.empty_like(w_in)
-            dist.all_to_all_single(w_out, w_in, group=self.group)
-            out.copy_(w_out.to(dev))
-        else:
-            dist.all_to_all_single(out, w_in, group=self.group)
+    def all_reduce_or(self, value: int) -> int:
+        """Bitwise OR of a 32-bit word over ranks (RCCL has no BOR: one MAX per bit)."""
+        bits = torch.tensor([(int(value) >> i) & 1 for i in range(32)], dtype=torch.int32,
+                            device=self._wire_device())
+        dist.all_reduce(bits, op=dist.ReduceOp.MAX, group=self.group)
+        return sum(int(b) << i for i, b in enumerate(bits.cpu().tolist()))
+
+    def all_gather_object(self, obj):
+        out = [None] * self.world
+        dist.all_gather_object(out, obj, group=self.group)
         return out
 
+    # -- point to point -----------------------------------------------------------
     def exchange_async(self, sends, recvs):
         """Start a point-to-point exchange; returns a handle with ``wait()``.
 
-        With RCCL the grouped send/recv runs on the communicator's stream,
-        which first waits for work already queued on the current stream; the
-        caller keeps queuing compute and calls ``wait()`` (the current stream
-        then waits for the transfer) right before consuming the receives. With
-        gloo the exchange completes before returning.
+        `sends` / `recvs` are lists of (peer, tensor); transfers between one
+        pair of ranks are matched in list order; peer == self must not appear
+        (callers copy locally). With RCCL the operations are one grouped launch
+        on the communicator's stream (every xGMI link busy at once), which
+        first waits for work already queued on the current stream; the caller
+        keeps queuing compute and calls ``wait()`` (the current stream then
+        waits for the transfer) right before consuming the receives. With gloo
+        the exchange completes before returning.
         """
-        if not self.device_native or (not sends and not recvs):
-            self.exchange(sends, recvs)
+        if not sends and not recvs:
+            return _Done()
+        if not self.device_native:
+            self._exchange_host(sends, recvs)
             return _Done()
         ops = [dist.P2POp(dist.isend, t.contiguous(), p, group=self.group) for p, t in sends]
         ops += [dist.P2POp(dist.irecv, t, p, group=self.group) for p, t in recvs]
         return _Pending(dist.batch_isend_irecv(ops), [t for _, t in sends])
 
     def exchange(self, sends, recvs):
-        """Point-to-point exchange: `sends` / `recvs` are lists of (peer, tensor).
+        self.exchange_async(sends, recvs).wait()
 
-        Transfers to/from the same peer are matched in list order; peer ==
-        self must not appear (callers copy locally). With RCCL the operations
-        are one grouped launch (every xGMI link busy at once); with gloo the
-        device tensors are staged through host buffers.
-        """
-        if not sends and not recvs:
-            return
-        if self.device_native:
-            ops = [dist.P2POp(dist.isend, t.contiguous(), p, group=self.group) for p, t in sends]
-            ops += [dist.P2POp(dist.irecv, t, p, group=self.group) for p, t in recvs]
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
-            return
+    def _exchange_host(self, sends, recvs):
         host_sends = [(p, t.contiguous().cpu() if t.is_cuda else t.contiguous()) for p, t in sends]
-        host_recvs = [(p, torch.empty(t.shape, dtype=t.dtype) if t.is_cuda else t, t)
-                      for p, t in recvs]
+        host_recvs = [(p, torch.empty(t.shape, dtype=t.dtype) if (t.is_cuda or not t.is_contiguous())
+                       else t, t) for p, t in recvs]
         ops = [dist.P2POp(dist.isend, t, p, group=self.group) for p, t in host_sends]
         ops += [dist.P2POp(dist.irecv, h, p, group=self.group) for p, h, _ in host_recvs]
         for w in dist.batch_isend_irecv(ops):
@@ -116,10 +156,70 @@ class Comm:
             if h is not t:
                 t.copy_(h)
 
-    def all_gather_object(self, obj):
-        out = [None] * self.world
-        dist.all_gather_object(out, obj, group=self.group)
-        return out
+    def exchange_bytes(self, sends: Sequence[tuple], recvs: Sequence[tuple]) -> List[bytes]:
+        """Small byte strings point to point: `sends` = [(peer, bytes)], `recvs` =
+        [(peer, nbytes)]; returns the received strings in `recvs` order."""
+        dev = self._wire_device()
+        st = [(p, torch.frombuffer(bytearray(b), dtype=torch.uint8).clone().to(dev)) for p, b in sends]
+        rt = [(p, torch.empty(n, dtype=torch.uint8, device=dev)) for p, n in recvs]
+        self.exchange(st, rt)
+        return [bytes(t.cpu().numpy().tobytes()) for _, t in rt]
+
+    def send_object(self, obj, peer: int):
+        """Host objects (CPU engines): blocking pickled send."""
+        dist.send_object_list([obj], dst=peer, group=self.group)
+
+    def recv_object(self, peer: int):
+        out = [None]
+        dist.recv_object_list(out, src=peer, group=self.group)
+        return out[0]
+
+    # -- liveness rendezvous on the process group's store -------------------------
+    @property
+    def store(self):
+        if self._store is None:
+            from torch.distributed.distributed_c10d import _get_default_store
+
+            self._store = dist.PrefixStore("sda", _get_default_store())
+        return self._store
+
+    def arrive(self, topic: str, who) -> None:
+        """Post "`who` reached `topic`" (non-blocking)."""
+        self.store.set(f"{topic}/at/{who}", b"1")
+
+    def decide(self, topic: str, expected: Sequence, deadline_s: Optional[float] = None,
+               all_or_nothing: bool = False, also: Sequence = ()) -> List:
+        """Collect arrivals: returns the members of `expected` that arrived -- as
+        soon as all have, else at the deadline -- and publishes them (plus
+        `also`, members the decider vouches for itself) for :meth:`decision`.
+        With `all_or_nothing` an incomplete set is published as empty."""
+        expected = list(expected)
+        deadline = time.monotonic() + (self.deadline_s if deadline_s is None else deadline_s)
+        keys = {w: f"{topic}/at/{w}" for w in expected}
+        live = expected
+        if expected:
+            try:
+                self.store.wait(list(keys.values()),
+                                timedelta(seconds=max(0.001, deadline - time.monotonic())))
+            except Exception:  # noqa: BLE001 - the store raises on timeout
+                live = [w for w in expected if self.store.check([keys[w]])]
+        if all_or_nothing and len(live) < len(expected):
+            live = []
+        pub = [str(w) for w in live] + [str(w) for w in also]
+        self.store.set(f"{topic}/live", ",".join(pub).encode() or b"-")
+        return live
+
+    def decision(self, topic: str, deadline_s: Optional[float] = None) -> List[str]:
+        """The published outcome of :meth:`decide`. Blocks until it is there; a
+        decider that never publishes (its process died) counts as "nobody"."""
+        t = self.deadline_s if deadline_s is None else deadline_s
+        try:
+            # the decider itself may wait a full deadline for stragglers first
+            self.store.wait([f"{topic}/live"], timedelta(seconds=2 * t + 2))
+        except Exception:  # noqa: BLE001 - the store raises on timeout
+            return []
+        v = self.store.get(f"{topic}/live").decode()
+        return [] if v == "-" else v.split(",")
 
 
 class _Done:

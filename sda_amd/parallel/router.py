@@ -1,96 +1,83 @@
-"""Committee routers: move sealed boxes from participant shards to clerk shards.
+"""Row movers: carry fixed-stride rows between ranks along a committee plan.
 
-Device: ciphertext arenas (fixed-stride slots) travel as contiguous byte ranges
-with their plaintext lengths -- grouped RCCL send/recv, no size pre-exchange
-needed because the slot stride is fixed by (dimension, modulus). The same plan
-moves just the 32-byte ephemeral-key headers ahead of the data, so the clerks'
-key agreement can run while the participants are still sealing. Host: lists
-of wire-format `Encryption` objects (gloo tests).
+Sealed boxes live in fixed-stride slots (the device ciphertext arena, or the
+host engines' length-prefixed rows), so the snapshot transpose needs no size
+pre-exchange: a transfer is a contiguous run of rows on both sides. The same
+plan moves the 32-byte ephemeral-key headers ahead of the data, so the clerks'
+key agreement overlaps the participants' sealing.
 """
 from __future__ import annotations
+
+from typing import Iterable, Sequence, Tuple
 
 import torch
 
 from .comm import Comm
-from .routing import plan
+from .routing import Plan
 
 
-class CommitteeRouter:
-    def __init__(self, comm: Comm, n: int, P: int):
-        self.comm, self.n, self.P = comm, n, P
-        self.sends, self.recvs = plan(comm.rank, comm.world, n, P)
-        self.bytes_sent = 0
+class RowRouter:
+    def __init__(self, comm: Comm, plan: Plan):
+        if plan.rank != comm.rank or plan.world != comm.world:
+            raise ValueError("plan does not belong to this rank")
+        self.comm, self.plan = comm, plan
 
-    # ---- generic row exchange ----------------------------------------------------
-    def row_ops(self, src, dst, base: int = 0, extra=()):
-        """Point-to-point ops moving rows of a clerk-major block of n*P rows.
+    def ops(self, pairs: Sequence[Tuple[torch.Tensor, torch.Tensor]], src_base: int = 0,
+            dst_base: int = 0, kind: str = "box"):
+        """Point-to-point ops moving the plan's rows of every (src, dst) pair.
 
-        `src` / `dst`: [M][R] tensors (M >= base + n*P); rows [base, base+n*P)
-        hold this rank's block (clerk c's participants at base + c*P ...).
-        `extra`: further (src, dst) row tensors moved alongside (e.g. lengths).
-        Local transfers are copied directly. Returns (sends, recvs, bytes_sent).
+        `src`: [>= src_base + n*P][R] clerk-major rows of this rank's
+        participants; `dst`: [>= dst_base + inbox_rows][R] inbox rows. Rows
+        that stay on this rank are copied directly (on the current stream).
+        Returns (sends, recvs) for :meth:`Comm.exchange_async`.
         """
-        P, me = self.P, self.comm.rank
-        pairs = [(src, dst)] + list(extra)
-        sends, recvs, sent = [], [], 0
-
-        def rows(t):
-            return slice(base + t.clerk * P + t.lo, base + t.clerk * P + t.hi)
-
-        for t in self.sends:
-            r = rows(t)
-            for s, d in pairs:
-                if t.peer == me:
-                    d[r].copy_(s[r])
-                else:
-                    sends.append((t.peer, s[r]))
-            if t.peer != me:
-                sent += src[r].numel() * src.element_size()
-        for t in self.recvs:
-            if t.peer == me:
+        me = self.comm.rank
+        sends, recvs = [], []
+        for t in self.plan.sends:
+            if t.count == 0:
                 continue
-            r = rows(t)
-            for _, d in pairs:
-                recvs.append((t.peer, d[r]))
-        return sends, recvs, sent
+            s = slice(src_base + t.src_row, src_base + t.src_row + t.count)
+            if t.peer == me:
+                d = slice(dst_base + t.dst_row, dst_base + t.dst_row + t.count)
+                for src, dst in pairs:
+                    if dst.data_ptr() != src.data_ptr() or s != d:
+                        dst[d].copy_(src[s])
+                continue
+            for src, _ in pairs:
+                rows = src[s]
+                sends.append((t.peer, rows))
+                self.comm.note(kind, "send", t.peer, t.clerk, rows.numel() * rows.element_size())
+        for t in self.plan.recvs:
+            if t.count == 0 or t.peer == me:
+                continue
+            d = slice(dst_base + t.dst_row, dst_base + t.dst_row + t.count)
+            for _, dst in pairs:
+                rows = dst[d]
+                recvs.append((t.peer, rows))
+                self.comm.note(kind, "recv", t.peer, t.clerk, rows.numel() * rows.element_size())
+        return sends, recvs
 
-    # ---- device arenas --------------------------------------------------------
-    def exchange(self, arena):
-        """Clerk-major arena [n*P] of this rank's participants -> inbox [n*P]."""
-        inbox, handle = self.exchange_async(arena)
-        handle.wait()
-        return inbox
 
-    def exchange_async(self, arena, inbox=None):
-        """Start the exchange; returns (inbox, handle): ``handle.wait()`` before
-        reading the inbox (the send arena must stay alive until then)."""
-        from ..ops.sealed import Arena
-
-        if arena.M != self.n * self.P:
-            raise ValueError("arena does not match the routing plan")
-        if inbox is None:
-            inbox = Arena(arena.M, arena.L, arena.modulus, arena.stride, arena.K,
-                          torch.empty_like(arena.ct), torch.empty_like(arena.pt_len))
-        elif inbox.M != arena.M or inbox.stride != arena.stride:
-            raise ValueError("inbox does not match the arena")
-        src = arena.ct.view(arena.M, arena.stride)
-        dst = inbox.ct.view(inbox.M, inbox.stride)
-        sends, recvs, sent = self.row_ops(
-            src, dst, extra=[(arena.pt_len.view(-1, 1), inbox.pt_len.view(-1, 1))])
-        handle = self.comm.exchange_async(sends, recvs)
-        self.bytes_sent = sent
-        return inbox, handle
-
-    # ---- host lists -------------------------------------------------------------
-    def exchange_host(self, boxes):
-        """boxes[p][c] (this rank's participants) -> inbox[c][p'] (P per clerk)."""
-        outgoing = {}
-        for t in self.sends:
-            outgoing.setdefault(t.peer, []).append(
-                (t.clerk, t.lo, t.hi, [boxes[p][t.clerk] for p in range(t.lo, t.hi)]))
-        everyone = self.comm.all_gather_object(outgoing)
-        inbox = [[None] * self.P for _ in range(self.n)]
-        for src, out in enumerate(everyone):
-            for c, lo, hi, items in out.get(self.comm.rank, []):
-                inbox[c][lo:hi] = items
-        return inbox
+def gather_rows_to(comm: Comm, root: int, pairs: Iterable[Tuple[torch.Tensor, torch.Tensor]],
+                   rows_per_rank: int, kind: str, senders: Sequence[int] | None = None):
+    """Every rank in `senders` (default: all) sends its `rows_per_rank` rows of
+    each `src` to `root`, which places rank r's at rows [r * rows_per_rank, ...)
+    of `dst`. Returns (sends, recvs)."""
+    me = comm.rank
+    senders = list(range(comm.world)) if senders is None else list(senders)
+    sends, recvs = [], []
+    for src, dst in pairs:
+        if me in senders:
+            if me == root:
+                dst[me * rows_per_rank:(me + 1) * rows_per_rank].copy_(src[:rows_per_rank])
+            else:
+                rows = src[:rows_per_rank]
+                sends.append((root, rows))
+                comm.note(kind, "send", root, -1, rows.numel() * rows.element_size())
+        if me == root:
+            for r in senders:
+                if r != root:
+                    rows = dst[r * rows_per_rank:(r + 1) * rows_per_rank]
+                    recvs.append((r, rows))
+                    comm.note(kind, "recv", r, -1, rows.numel() * rows.element_size())
+    return sends, recvs

@@ -6,12 +6,12 @@ as waves of W participants through the device engine's participate+clerk
 phase. Only the clerks' running sums (n x B) and the recipient's mask sum (D)
 persist between waves; each wave's shares, arenas and decoded values are
 recycled. The running sums are checkpointed every few waves so a stopped
-run resumes where it stopped (SURVEY 5.4: the reference's durability is its
+run resumes where it stopped (the reference's durability is its
 stores; on the GPU path it is these accumulators).
 
-In a multi-GPU round each rank streams its own participant range and the
-committee router moves every wave's boxes to the clerks' ranks; the sums are
-reduced to rank 0 once, at the end.
+In a multi-GPU round each rank streams its own participant range, every wave's
+sealed boxes travel to the clerks' ranks, and the clerks' sealed results go to
+the recipient's rank once, at the end.
 """
 from __future__ import annotations
 
@@ -36,23 +36,21 @@ class StreamResult:
 
 class StreamingAggregator:
     def __init__(self, engine: DeviceAggregator, wave: int = 64,
-                 checkpoint: Optional[str] = None, checkpoint_every: int = 8,
-                 inner_waves: int = 4):
+                 checkpoint: Optional[str] = None, checkpoint_every: int = 8):
         if wave <= 0:
             raise ValueError("wave must be positive")
         self.engine = engine
-        self.inner_waves = max(1, inner_waves)
         self.wave = wave
         self.checkpoint = checkpoint
         self.every = max(1, checkpoint_every)
 
     # ---- checkpoints ---------------------------------------------------------
-    def _fingerprint(self, total: int, live) -> str:
+    def _fingerprint(self, total: int, live, rows) -> str:
         spec = self.engine.spec
         return json.dumps({"dimension": spec.dimension, "modulus": spec.field_modulus,
                            "sharing": spec.sharing.to_wire(), "masking": spec.masking.to_wire(),
-                           "participants": total, "wave": self.wave, "live": list(live)},
-                          sort_keys=True)
+                           "participants": total, "wave": self.wave, "live": list(live),
+                           "rows": list(rows)}, sort_keys=True)
 
     def _save(self, acc, mask_acc, next_wave: int, fp: str):
         from safetensors.torch import save_file
@@ -79,24 +77,30 @@ class StreamingAggregator:
 
     # ---- the round -------------------------------------------------------------
     def run(self, total: int, make_wave: Callable[[int, int, int], torch.Tensor],
-            clerks: Optional[Sequence[int]] = None, reducer=None, router_for=None,
+            clerks: Optional[Sequence[int]] = None, reducer=None, committee=None,
             owner_base: int = 0, resume: bool = True, stop_after: Optional[int] = None,
             check: bool = True) -> StreamResult:
         """Aggregate `total` participants delivered by ``make_wave(w, first, count)``.
 
-        `router_for(count)` returns the committee router for a wave of `count`
-        participants (multi-GPU), `reducer` sums the accumulators over ranks.
-        `stop_after` ends the run after that many waves of this call
-        (checkpoint kept) -- used to exercise resume.
+        Multi-GPU: `committee` (a :class:`sda_amd.parallel.device_round.DeviceCommittee`)
+        routes every wave's boxes to the clerks' ranks and gathers the sealed
+        results at the end; `reducer` is the ``owner`` layout's plaintext
+        reduce. This rank's running sums -- one row per clerk it accumulates
+        for, plus on the recipient's rank the mask sum -- are what the
+        checkpoints hold. `stop_after` ends the run after that many waves of
+        this call (checkpoint kept) -- used to exercise resume.
         """
         eng = self.engine
         live = eng._live(clerks)
         B, D, dev = eng.spec.batches, eng.spec.dimension, eng.device
         waves = (total + self.wave - 1) // self.wave
-        fp = self._fingerprint(total, live)
-        acc = torch.zeros(len(live), B, dtype=torch.int64, device=dev)
-        mask_acc = (torch.zeros(D, dtype=torch.int64, device=dev)
-                    if eng.spec.masking.has_mask() else None)
+        # accumulator rows: the live clerks (one GPU / owner) or this rank's hosted ones
+        rows = list(live) if committee is None else [c for c in committee.hosted if c in live]
+        fp = self._fingerprint(total, live, rows)
+        acc = torch.zeros(len(rows), B, dtype=torch.int64, device=dev)
+        has_mask = eng.spec.masking.has_mask()
+        keeps_mask = has_mask and (committee is None or committee.comm.rank == committee.ROOT)
+        mask_acc = torch.zeros(D, dtype=torch.int64, device=dev) if keeps_mask else None
         start = 0
         if resume:
             state = self._load(fp)
@@ -108,27 +112,30 @@ class StreamingAggregator:
         err = eng.new_error_word()
         marks: list = []
         eng._mark(marks, "start")
-        rk = None  # recipient key agreement: queued behind the first wave's
+        ctx = None
+        rk = None  # recipient / result key agreement: queued behind the first wave's
         done = 0
         for w in range(start, waves):
             first = w * self.wave
             count = min(self.wave, total - first)
             x = make_wave(w, first, count)
-            if router_for is not None and count >= 2:
-                # committee layout: the exchange is pipelined inside the wave
-                comb, msum = eng.participate_and_clerk_pipelined(
-                    x, live, err, router_for, waves=min(self.inner_waves, count),
-                    owner_base=owner_base + first)
+            if committee is not None:
+                part, mask_arena = committee.participate_exchange_clerk(
+                    x, live, err, owner_base=owner_base + first)
+                if ctx is None:
+                    ctx = committee.begin(live, err)
+                    ctx.mask_acc = mask_acc
+                committee.ship_masks(ctx, mask_arena, err)
+                for c, v in part.items():
+                    acc[rows.index(c)] += v
+                mask_acc = ctx.mask_acc
             else:
-                router = router_for(count) if router_for is not None else None
-                comb, msum = eng.participate_and_clerk(x, live, err,
-                                                       owner_base=owner_base + first,
-                                                       router=router)
-            if rk is None:
-                rk = eng.prepare_reveal(live, err)
-            acc += comb
-            if mask_acc is not None:
-                mask_acc += msum
+                comb, msum = eng.participate_and_clerk(x, live, err, owner_base=owner_base + first)
+                if rk is None:
+                    rk = eng.prepare_reveal(live, err)
+                acc += comb
+                if mask_acc is not None:
+                    mask_acc += msum
             done += 1
             last = w == waves - 1
             if self.checkpoint and ((w + 1) % self.every == 0 or last or
@@ -139,17 +146,26 @@ class StreamingAggregator:
                 return StreamResult(None, live, done, start)
         eng._mark(marks, "waves")
         m = eng.m
-        combined = torch.remainder(acc, m).to(torch.int32)
-        mask_sum = torch.remainder(mask_acc, m).to(torch.int32) if mask_acc is not None else None
-        if reducer is not None:
-            combined, mask_sum = eng.reduce_partials(combined, mask_sum, reducer, marks)
-            if combined is None:
+        if committee is not None:
+            if ctx is None:  # resumed past the last wave
+                ctx = committee.begin(live, err)
+                ctx.mask_acc = mask_acc
+            out, used = committee.finish(ctx, {c: acc[i] for i, c in enumerate(rows)}, err, marks)
+            if check:
                 self._check(err)
-                return StreamResult(None, live, done, start)
-        out = eng.reveal(combined, mask_sum, live, err, marks=marks, keys=rk)
-        if check:
-            self._check(err)
-        res = StreamResult(out, live, done, start)
+            res = StreamResult(out, used, done, start)
+        else:
+            combined = torch.remainder(acc, m).to(torch.int32)
+            mask_sum = torch.remainder(mask_acc, m).to(torch.int32) if mask_acc is not None else None
+            if reducer is not None:
+                combined, mask_sum = eng.reduce_partials(combined, mask_sum, reducer, marks)
+                if combined is None:
+                    self._check(err)
+                    return StreamResult(None, live, done, start)
+            out = eng.reveal(combined, mask_sum, live, err, marks=marks, keys=rk)
+            if check:
+                self._check(err)
+            res = StreamResult(out, live, done, start)
         if eng.time_stages:
             torch.cuda.synchronize()
             for (a, ea), (b, eb) in zip(marks, marks[1:]):

@@ -27,15 +27,28 @@ def _worker(rank, world, port, name, layout, q):
     try:
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        from sda_amd.models.schemes import PSS_4_8_3, Additive, AggregationSpec, FullMask
+        from sda_amd.models.schemes import (PSS_4_8_3, Additive, AggregationSpec, ChaChaMask,
+                                            FullMask)
         from sda_amd.parallel import DistributedAggregator
 
         D, P, m = 5000, 6, 433
+        if name == "bigmod":
+            m = 2 ** 31 - 1
         spec = {"fullmask": AggregationSpec(D, m, Additive(3, m), FullMask(m)),
                 "additive2": AggregationSpec(D, m, Additive(2, m)),
+                "chacha": AggregationSpec(D, m, Additive(3, m), ChaChaMask(m, D)),
+                "bigmod": AggregationSpec(D, m, Additive(4, m), FullMask(m)),
                 "pss": AggregationSpec(D, m, PSS_4_8_3)}[name]
         agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", 0),
-                                    layout="committee" if layout == "stream" else layout)
+                                    layout="owner" if layout == "owner" else "committee",
+                                    waves=3, force_pipeline=True, deadline_s=30.0)
+        # key custody: only the hosted clerks' secret keys (+ the recipient's on rank 0)
+        if layout != "owner":
+            from sda_amd.parallel.routing import hosted_clerks
+
+            held = [i for i in range(spec.n_clerks + 1) if agg.engine.keys.holds(i)]
+            want = hosted_clerks(rank, world, spec.n_clerks) + ([spec.n_clerks] if rank == 0 else [])
+            assert held == want, (held, want)
 
         def inputs(r):
             g = torch.Generator().manual_seed(99 + r)
@@ -48,6 +61,7 @@ def _worker(rank, world, port, name, layout, q):
         else:
             res = agg.run_round(inputs(rank).cuda())
         if rank == 0:
+            assert res.output is not None
             ref = torch.remainder(sum(inputs(r).to(torch.int64).sum(0) for r in range(world)), m)
             q.put(("ok", bool(torch.equal(res.output.cpu().to(torch.int64), ref))))
         else:
@@ -61,6 +75,11 @@ def _worker(rank, world, port, name, layout, q):
                                                (2, "pss", "committee"),
                                                (2, "fullmask", "owner"),
                                                (3, "additive2", "committee"),
+                                               (4, "chacha", "committee"),
+                                               # sums of waves of values below m = 2^31 - 1
+                                               # must not wrap (pipelined waves, world 1 and 2)
+                                               (1, "bigmod", "committee"),
+                                               (2, "bigmod", "committee"),
                                                (3, "fullmask", "stream")])
 def test_distributed_device_ranks_one_gpu(cuda, world, name, layout):
     ctx = mp.get_context("spawn")
@@ -98,3 +117,28 @@ def test_bench_over_rccl_single_rank(cuda, layout):
     assert out.returncode == 0, out.stderr[-3000:]
     line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 1 and line["value"] > 0
+    assert line["hbm_high_water_bytes"] > 0 and line["xgmi"]["bytes_sent_per_rank_per_round"] == 0
+    assert ("committee" in line["config"]["parallelism"]) == (layout == "committee")
+    assert ("non-private upper bound" in line["config"]["parallelism"]) == (layout == "owner")
+
+
+@pytest.mark.parametrize("dist", [False, True])
+def test_bench_fails_on_a_corrupted_box_in_a_timed_step(cuda, dist):
+    """A flipped ciphertext bit in a timed (unchecked) step must fail the run:
+    the error words of all timed steps are OR-ed on device and read once."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    tail = ["--gpus", "1", "--steps", "3", "--warmup", "1", "--participants", "24", "--dim",
+            "60000", "--corrupt-step", "1"]
+    if dist:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               os.path.join(root, "bench.py"), "--force-dist"] + tail
+    else:
+        cmd = [sys.executable, os.path.join(root, "bench.py")] + tail
+    out = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
+    assert out.returncode != 0
+    assert "MAC verification failed" in out.stderr, out.stderr[-2000:]
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]

@@ -1,49 +1,106 @@
-"""Committee routing plan properties (sda_amd/parallel/routing.py)."""
+"""Committee plan properties (CPU): the snapshot transpose as a uniform all-to-all.
+
+The reference transposes participations P x n into clerk jobs n x P
+(server/src/snapshot.rs:11-27, server/src/stores.rs:86-101); the plan must
+deliver every box exactly once, keep the clerks' load balanced, and keep two
+clerks' shares of one participant off the same rank whenever there are at least
+as many ranks as clerks.
+"""
 import itertools
 
 import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
 
-from sda_amd.parallel.routing import destinations, plan
+from sda_amd.parallel.routing import hosted_clerks, hosts, lead, piece, plan
+
+CASES = [(1, 3, 7), (2, 3, 5), (3, 3, 4), (4, 3, 5), (8, 3, 1000), (8, 8, 125), (4, 8, 6),
+         (3, 8, 5), (8, 26, 3), (5, 2, 9), (7, 3, 1), (8, 3, 2)]
 
 
-CASES = [(w, n, P) for w in (1, 2, 3, 4, 8) for n in (2, 3, 5, 8) for P in (1, 7, 1000)]
+def _deliveries(world, n, P):
+    """{(dst, inbox_row): (src, clerk, participant)} from every rank's sends."""
+    got = {}
+    for s in range(world):
+        for t in plan(s, world, n, P).sends:
+            for i in range(t.count):
+                key = (t.peer, t.dst_row + i)
+                assert key not in got, "two boxes land on one inbox row"
+                got[key] = (s, t.clerk, t.src_row - t.clerk * P + i)
+    return got
 
 
 @pytest.mark.parametrize("world,n,P", CASES)
-def test_plan_coverage_and_balance(world, n, P):
-    plans = [plan(r, world, n, P) for r in range(world)]
-    # sends and receives match pairwise
-    sent = sorted((r, t.peer, t.clerk, t.lo, t.hi) for r, (s, _) in enumerate(plans) for t in s)
-    recv = sorted((t.peer, r, t.clerk, t.lo, t.hi) for r, (_, rv) in enumerate(plans) for t in rv)
-    assert sent == recv
-    for r, (sends, recvs) in enumerate(plans):
-        # every source's P boxes of every clerk are sent exactly once
-        for c in range(n):
-            covered = sorted((t.lo, t.hi) for t in sends if t.clerk == c)
-            assert covered[0][0] == 0 and covered[-1][1] == P
-            assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
-        # balance: each clerk region of the inbox is exactly [0, P)
-        for c in range(n):
-            got = sorted((t.lo, t.hi) for t in recvs if t.clerk == c)
-            assert got[0][0] == 0 and got[-1][1] == P
-            assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
+def test_every_box_delivered_once_and_sends_match_recvs(world, n, P):
+    got = _deliveries(world, n, P)
+    assert sorted(got.values()) == sorted(itertools.product(range(world), range(n), range(P)))
+    # receives mirror the sends exactly
+    for r in range(world):
+        pl = plan(r, world, n, P)
+        mine = sorted((t.peer, t.clerk, t.src_row, t.dst_row, t.count) for t in pl.recvs if t.count)
+        theirs = sorted((s, t.clerk, t.src_row, t.dst_row, t.count)
+                        for s in range(world) for t in plan(s, world, n, P).sends
+                        if t.peer == r and t.count)
+        assert mine == theirs
+        rows = sorted(row for (d, row) in got if d == r)
+        assert rows == list(range(pl.inbox_rows))  # the inbox is dense
 
 
-@pytest.mark.parametrize("world,n", [(w, n) for w in (4, 5, 8, 16) for n in (2, 3, 5, 7) if w - 1 >= n])
-def test_plan_privacy(world, n):
-    for s in range(world):
-        groups = destinations(s, world, n)
-        flat = list(itertools.chain(*groups))
-        assert s not in flat                      # never back to the participants' own GPU
-        assert len(flat) == len(set(flat))        # one clerk per destination per source
-        assert sorted(flat) == sorted(set(range(world)) - {s})  # all links used
+@pytest.mark.parametrize("world,n,P", CASES)
+def test_balance_and_uniform_links(world, n, P):
+    total = n * P
+    for r in range(world):
+        pl = plan(r, world, n, P)
+        per_source = sum(s.count for s in pl.segments)
+        assert per_source in (total // world, -(-total // world))
+        assert pl.inbox_rows == world * per_source
+        # every source sends this rank the same number of boxes: a uniform all-to-all
+        by_src = {}
+        for t in pl.recvs:
+            by_src[t.peer] = by_src.get(t.peer, 0) + t.count
+        assert set(by_src.values()) == ({per_source} if per_source else set())
 
 
-def test_eight_gpus_three_clerks_link_load():
-    # config 2 weak-scaled to 8 GPUs: at most ceil(P/2) boxes per link
-    P = 1000
-    sends, _ = plan(0, 8, 3, P)
-    per_peer = {}
-    for t in sends:
-        per_peer[t.peer] = per_peer.get(t.peer, 0) + t.count
-    assert len(per_peer) == 7 and max(per_peer.values()) <= 500
+@pytest.mark.parametrize("world,n,P", CASES)
+def test_custody_and_privacy(world, n, P):
+    got = _deliveries(world, n, P)
+    for r in range(world):
+        segs = piece(r, world, n, P)
+        # a rank only receives boxes of clerks it is a host of
+        assert {s.clerk for s in segs} <= set(hosted_clerks(r, world, n))
+        seen = {}
+        for (d, _), (src, c, p) in got.items():
+            if d == r:
+                seen.setdefault((src, p), set()).add(c)
+        if n <= world:
+            assert len(hosted_clerks(r, world, n)) <= 2
+            # no rank ever holds two clerks' shares of one participant
+            assert all(len(cs) == 1 for cs in seen.values())
+    for c in range(n):
+        hs = hosts(c, world, n)
+        assert hs and lead(c, world, n) == hs[0] and hs == sorted(hs)
+        # the hosts' segments partition the clerk's P slots
+        cover = sorted((s.lo, s.hi) for r in hs for s in piece(r, world, n, P) if s.clerk == c)
+        flat = [x for lo, hi in cover for x in range(lo, hi)]
+        assert flat == list(range(P))
+
+
+def test_single_rank_inbox_is_the_arena():
+    pl = plan(0, 1, 3, 10)
+    assert [(s.clerk, s.lo, s.hi) for s in pl.segments] == [(0, 0, 10), (1, 0, 10), (2, 0, 10)]
+    assert all(t.src_row == t.dst_row for t in pl.sends)
+
+
+def test_eight_ranks_eight_clerks_is_one_clerk_per_rank():
+    for r in range(8):
+        assert hosted_clerks(r, 8, 8) == [r]
+        assert [(s.clerk, s.lo, s.hi) for s in piece(r, 8, 8, 125)] == [(r, 0, 125)]
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.integers(1, 9), st.integers(2, 12), st.integers(1, 40))
+def test_plan_properties_random(world, n, P):
+    got = _deliveries(world, n, P)
+    assert len(got) == world * n * P
+    for c in range(n):
+        assert hosts(c, world, n)
