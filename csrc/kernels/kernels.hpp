@@ -155,9 +155,15 @@ void launch_decode(int M, int K, int L, uint32_t m, int value_bytes, const uint8
 // out [R][L] = sum_p values mod m.
 void launch_locate_tiles(int M, int S, int L, const uint32_t* pre, const uint32_t* totals,
                          uint32_t* tile_sub, hipStream_t s);
+// `redo` (may be null): one zeroed scratch word. With it and m <= 8192 the lean
+// kernel (sums of zigzag codes, no per-element decode) runs first and the
+// generic one only if a stream is not canonical (long or negative varints);
+// needs Pg * 16383 < 2^32 as well.
 void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* pt, uint64_t stride,
                        const uint32_t* pt_len, int S, const uint32_t* pre, const uint32_t* tile_sub,
-                       uint32_t* part, uint32_t* out, uint32_t* err, hipStream_t s);
+                       uint32_t* part, uint32_t* out, uint32_t* err, uint32_t* redo, hipStream_t s);
+// Lean clerk decode (default on; 0 = generic kernel only) -- benchmarking switch.
+void set_decode_lean(int mode);
 // Column sums mod m: out[g][l] = sum_r vals[g][r][l] mod m.
 void launch_colsum(int G, int R, int L, uint32_t m, int value_bytes, const void* vals,
                    uint32_t* out, hipStream_t s);

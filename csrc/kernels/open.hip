@@ -202,31 +202,175 @@ __global__ void __launch_bounds__(kBlock)
     k_decode_sum(int L, int P, int Pg, ModParams mp, const uint8_t* __restrict__ pt,
                  uint64_t stride, const uint32_t* __restrict__ pt_len, int S,
                  const uint32_t* __restrict__ pre, const uint32_t* __restrict__ tile_sub,
-                 uint32_t* __restrict__ part, uint32_t* err) {
+                 uint32_t* __restrict__ part, uint32_t* err, const uint32_t* gate) {
   __shared__ uint32_t acc[kSumAcc];
   __shared__ uint32_t info[kBlock][4];
+  // behind the lean kernel: only if it met a stream it does not handle
+  if (gate != nullptr && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
   decode_sum_body<kFast16, AddSink>(acc, info, L, P, Pg, mp, pt, stride, pt_len, S, pre, tile_sub,
                                     part, err);
 }
 
+// ---------------------------------------- clerk decode + combine, lean form
+// The common case -- canonical shares below 8192, i.e. every varint one or two
+// bytes long and non-negative -- needs no per-element decode at all: the zigzag
+// code of an element is the sum of its bytes' contributions
+//     (byte & 0x7f) << (7 if the previous byte is a continuation byte else 0)
+// so every byte position adds its contribution at the rank of the element it
+// belongs to (a continuation byte has the rank of the terminator after it), and
+// the accumulator ends up holding sum(z) = 2 * sum(value); k_sum_slabs halves.
+// Same tiling, ranks and accumulator window as k_decode_sum; ~1/3 of its VALU
+// work. A lane that sees anything else (three-byte varints, an odd = negative
+// code) raises `redo`: the generic kernel, launched right after and gated on
+// that word, then recomputes every slab (foreign encoders such as the
+// reference's Rust-`%` shares, additive.rs:47, take that path).
+//
+// Ownership at range edges (ranges are cut at 1 KiB sub-chunks, which may split
+// a two-byte varint): an element belongs to the range holding its terminator. A
+// lane therefore drops a continuation byte in its last valid position and adds
+// the continuation byte just before its first valid position (from its own
+// words, or from the previous lane's last byte).
+SDA_DEV uint32_t spread4(uint32_t bits4) {  // 4 bits -> 0xff per set bit, byte k <- bit k
+  return ((bits4 * 0x00204081u) & 0x01010101u) * 0xffu;
+}
+
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+    k_decode_sum_z(int L, int P, int Pg, const uint8_t* __restrict__ pt, uint64_t stride,
+                   const uint32_t* __restrict__ pt_len, int S, const uint32_t* __restrict__ pre,
+                   const uint32_t* __restrict__ tile_sub, uint32_t* __restrict__ part,
+                   uint32_t* redo, uint32_t* err) {
+  constexpr int kWaveBytes = 64 * 64;
+  __shared__ uint32_t acc[kSumAcc];
+  __shared__ uint32_t info[kBlock][4];
+  const int t = blockIdx.x, r = blockIdx.y, g = blockIdx.z, R = gridDim.y;
+  const int T = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t E0 = (uint32_t)t * kSumTile;
+  const uint32_t W = min((uint32_t)kSumTile, (uint32_t)L - E0);
+  for (int i = tid; i < kSumAcc; i += kBlock) acc[i] = 0;
+  const int pbeg = g * Pg, pend = min(P, pbeg + Pg);
+  uint32_t bad = 0;      // bit 7 / bit 0 of any byte: not a canonical short stream
+  bool malformed = false;
+  for (int b0 = pbeg; b0 < pend; b0 += kBlock) {
+    const int cnt = min(kBlock, pend - b0);
+    __syncthreads();  // previous batch's info reads done (and acc zeroed)
+    if (tid < cnt) {
+      const size_t j = (size_t)r * P + b0 + tid;
+      const uint32_t s0 = tile_sub[j * (T + 1) + t];
+      info[tid][0] = s0;
+      info[tid][1] = tile_sub[j * (T + 1) + t + 1];
+      info[tid][2] = s0 < (uint32_t)S ? pre[j * S + s0] : 0u;
+      info[tid][3] = pt_len[j];
+    }
+    __syncthreads();
+    for (int i = wave; i < cnt; i += kWaves) {
+      const uint32_t s0 = info[i][0];
+      if (s0 >= (uint32_t)S) continue;  // fewer elements than the tile start: flagged by the totals
+      const uint32_t s1 = min(info[i][1], (uint32_t)S - 1);
+      const int64_t N = info[i][3];
+      const uint8_t* gmsg = pt + ((size_t)r * P + b0 + i) * stride + 48;
+      const int64_t qs = max((int64_t)0, (int64_t)s0 * kSubBytes - 32);
+      const int64_t qe = min(N, ((int64_t)s1 + 1) * kSubBytes - 32);
+      uint32_t rank = info[i][2];
+      for (int64_t c0 = (int64_t)s0 * kSubBytes - 32; c0 < qe; c0 += kWaveBytes) {
+        const int64_t p0 = c0 + 64 * lane;
+        uint32_t w[16];
+        load_lane_bytes(w, gmsg, p0, qe);
+        uint32_t pm1 = __shfl_up(w[15], 1, 64);  // the 4 bytes before this lane's (raw)
+        if (lane == 0) {
+          pm1 = 0;
+          if (p0 - 4 >= 0 && p0 - 4 < N) pm1 = *reinterpret_cast<const uint32_t*>(gmsg + p0 - 4);
+        }
+        const int lo = (int)max((int64_t)0, qs - p0);
+        const int hi = (int)min((int64_t)64, qe - p0);
+        // a message must end on a terminator
+        if (hi > lo && p0 + hi == N && (gmsg[N - 1] & 0x80)) malformed = true;
+        uint32_t tw[16];  // valid terminators, in place (bit 7 of their byte)
+        if (lo > 0 || hi < 64) {
+          uint64_t K = byte_range_mask(lo, hi);  // bytes that contribute
+          const uint64_t V = K;                  // bytes whose terminators count
+          if (hi > lo) {
+            const uint64_t craw = ~term_mask64(w);
+            if (lo > 0) K |= craw & (1ull << (lo - 1));
+            K &= ~(craw & (1ull << (hi - 1)));
+          }
+          if (lo > 0 || hi <= lo) pm1 = 0;  // the byte before this lane is not its to add
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const uint32_t k4 = (uint32_t)(K >> (4 * q)) & 15u, v4 = (uint32_t)(V >> (4 * q)) & 15u;
+            tw[q] = ~w[q] & spread4(v4) & 0x80808080u;
+            w[q] &= spread4(k4);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) tw[q] = ~w[q] & 0x80808080u;
+          // a continuation byte in the last position belongs to the next lane's element
+          w[15] &= ~((uint32_t)((int32_t)w[15] >> 31) & 0xff000000u);
+        }
+        uint32_t c = 0;
+        {
+          uint32_t wp = pm1;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const uint32_t pcb = __builtin_amdgcn_alignbyte(w[q], wp, 3) & 0x80808080u;
+            bad |= w[q] & pcb;                                  // continuation after continuation
+            bad |= w[q] & 0x01010101u & ~(pcb >> 7);            // odd first byte: a negative value
+            c += (uint32_t)__popc(tw[q]);
+            wp = w[q];
+          }
+          bad |= (pm1 >> 24) & (pm1 >> 31) & 1u;                // ... of the byte before
+          bad |= (pm1 >> 16) & (pm1 >> 24) & 0x80u;             // two continuation bytes before it
+        }
+        const uint32_t incl = wave_incl_scan(c);
+        const uint32_t total = __shfl(incl, 63, 64);
+        uint32_t* a = acc + (rank + kSumMargin - E0 + (incl - c));
+        atomicAdd(a, ((pm1 >> 24) & 0x7fu) & (0u - (pm1 >> 31)));
+        uint32_t wp = pm1;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const uint32_t x = w[q];
+          const uint32_t sh4 = ((__builtin_amdgcn_alignbyte(x, wp, 3) & 0x80808080u) >> 7) * 7u;
+          const uint32_t w7 = x & 0x7f7f7f7fu, tq = tw[q];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            atomicAdd(a, ((w7 >> (8 * u)) & 0xffu) << ((sh4 >> (8 * u)) & 0xffu));
+            a += (tq >> (8 * u + 7)) & 1u;
+          }
+          wp = x;
+        }
+        rank += total;
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t* out = part + ((size_t)g * R + r) * L + E0;
+  for (uint32_t i = tid; i < W; i += kBlock) out[i] = acc[kSumMargin + i];
+  if (bad) atomicOr(redo, 1u);
+  if (malformed) atomicOr(err, kErrMalformed);
+}
+
 // out[x] = sum_g part[g][x] mod m   (x < X = rows * L)
+// `zform` (may be null): *zform == 0 means the slabs hold sums of zigzag codes
+// (2 * value, from k_decode_sum_z) and are halved first.
 __global__ void __launch_bounds__(kBlock)
     k_sum_slabs(int G, int64_t X, ModParams mp, const uint32_t* __restrict__ part,
-                uint32_t* __restrict__ out) {
+                uint32_t* __restrict__ out, const uint32_t* zform) {
   const int64_t x = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
   if (x >= X) return;
+  const int sh = (zform != nullptr && *zform == 0u) ? 1 : 0;
   if (x + 4 <= X && (X % 4) == 0) {
     uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     for (int g = 0; g < G; ++g) {
       const uint4 q = *reinterpret_cast<const uint4*>(part + g * X + x);
       a0 += q.x; a1 += q.y; a2 += q.z; a3 += q.w;
     }
-    *reinterpret_cast<uint4*>(out + x) = make_uint4(mod64(a0, mp), mod64(a1, mp), mod64(a2, mp), mod64(a3, mp));
+    *reinterpret_cast<uint4*>(out + x) = make_uint4(mod64(a0 >> sh, mp), mod64(a1 >> sh, mp),
+                                                     mod64(a2 >> sh, mp), mod64(a3 >> sh, mp));
   } else {
     for (int64_t y = x; y < min(X, x + 4); ++y) {
       uint64_t a = 0;
       for (int g = 0; g < G; ++g) a += part[g * X + y];
-      out[y] = mod64(a, mp);
+      out[y] = mod64(a >> sh, mp);
     }
   }
 }
@@ -294,6 +438,9 @@ __global__ void k_sub_mod(int D, uint32_t m, const uint32_t* __restrict__ a,
 
 }  // namespace
 
+static int g_decode_lean = 1;
+void set_decode_lean(int mode) { g_decode_lean = mode; }
+
 void launch_decode(int M, int K, int L, uint32_t m, int value_bytes, const uint8_t* pt,
                    uint64_t stride, const uint32_t* pt_len, const uint32_t* elem_start,
                    void* vals, uint32_t* err, hipStream_t s) {
@@ -318,22 +465,29 @@ void launch_locate_tiles(int M, int S, int L, const uint32_t* pre, const uint32_
 
 void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* pt, uint64_t stride,
                        const uint32_t* pt_len, int S, const uint32_t* pre, const uint32_t* tile_sub,
-                       uint32_t* part, uint32_t* out, uint32_t* err, hipStream_t s) {
+                       uint32_t* part, uint32_t* out, uint32_t* err, uint32_t* redo, hipStream_t s) {
   if (R <= 0 || P <= 0 || L <= 0 || Pg <= 0 || m == 0) return;
   const ModParams mp = make_mod_params(m);
   const int T = (L + kSumTile - 1) / kSumTile;
   const int G = (P + Pg - 1) / Pg;
   dim3 grid(T, R, G);
+  // lean kernel first where every canonical value is a 1- or 2-byte varint; the
+  // generic one then runs only if `redo` was raised (it rewrites every slab)
+  const bool lean = g_decode_lean && redo != nullptr && m <= 8192u;
+  if (lean)
+    hipLaunchKernelGGL(k_decode_sum_z, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S, pre,
+                       tile_sub, part, redo, err);
+  const uint32_t* gate = lean ? redo : nullptr;
   if (m < 65536u)
     hipLaunchKernelGGL(k_decode_sum<true>, grid, dim3(kBlock), 0, s, L, P, Pg, mp, pt, stride,
-                       pt_len, S, pre, tile_sub, part, err);
+                       pt_len, S, pre, tile_sub, part, err, gate);
   else
     hipLaunchKernelGGL(k_decode_sum<false>, grid, dim3(kBlock), 0, s, L, P, Pg, mp, pt, stride,
-                       pt_len, S, pre, tile_sub, part, err);
+                       pt_len, S, pre, tile_sub, part, err, gate);
   const int64_t X = (int64_t)R * L;
   const int64_t threads = (X + 3) / 4;
   hipLaunchKernelGGL(k_sum_slabs, dim3((unsigned)((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                     G, X, mp, part, out);
+                     G, X, mp, part, out, gate);
 }
 
 void launch_colsum(int G, int R, int L, uint32_t m, int value_bytes, const void* vals,

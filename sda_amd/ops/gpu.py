@@ -294,15 +294,26 @@ def locate_tiles(pre: torch.Tensor, totals: torch.Tensor, L: int, tile_sub: torc
     _gpu().locate_tiles(M, S, L, _ptr(pre), _ptr(totals), _ptr(tile_sub), _stream())
 
 
+def decode_sum_group_limit(modulus: int) -> int:
+    """Most participants one decode-sum accumulator (u32) may add up: sums of
+    canonical values, or of 14-bit zigzag codes on the lean path (m <= 8192)."""
+    per = max(modulus - 1, 16383) if modulus <= 8192 else modulus - 1
+    return max(1, (2 ** 32 - 1) // max(1, per))
+
+
 def decode_sum(rows: int, P: int, Pg: int, L: int, modulus: int, pt, stride, pt_len, pre,
-               tile_sub, part, out, err):
-    """out[r] = sum_p decode(message r*P + p) mod m (fused decode + combine)."""
+               tile_sub, part, out, err, redo=None):
+    """out[r] = sum_p decode(message r*P + p) mod m (fused decode + combine).
+
+    `redo`: a zeroed int32 scratch word enabling the lean kernel (m <= 8192)."""
     M = rows * P
     S = pre.shape[1]
     if modulus <= 0:
         raise ValueError("decode_sum needs a modulus")
-    if Pg < 1 or Pg * (modulus - 1) >= 2 ** 32:
-        raise ValueError("decode_sum: Pg * (m - 1) must fit the u32 accumulators")
+    if Pg < 1 or Pg > decode_sum_group_limit(modulus):
+        raise ValueError("decode_sum: the group's sums must fit the u32 accumulators")
+    if redo is not None:
+        _check(redo, "redo", torch.int32, numel=1)
     groups = (P + Pg - 1) // Pg
     _check(pt, "pt", torch.uint8, min_numel=M * stride)
     _check(pt_len, "pt_len", torch.int32, numel=M)
@@ -312,7 +323,8 @@ def decode_sum(rows: int, P: int, Pg: int, L: int, modulus: int, pt, stride, pt_
     _check(out, "out", torch.int32, numel=rows * L)
     _check(err, "err", torch.int32, numel=1)
     _gpu().decode_sum(rows, P, Pg, L, modulus, _ptr(pt), stride, _ptr(pt_len), S, _ptr(pre),
-                      _ptr(tile_sub), _ptr(part), _ptr(out), _ptr(err), _stream())
+                      _ptr(tile_sub), _ptr(part), _ptr(out), _ptr(err),
+                      _ptr(redo) if redo is not None else 0, _stream())
 
 
 def colsum(vals: torch.Tensor, modulus: int, out: torch.Tensor):

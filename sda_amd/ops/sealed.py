@@ -241,10 +241,11 @@ def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
     G.locate_tiles(pre, totals, L, tile_sub)
     # participant groups: ~4k blocks fill the chip; u32 accumulators bound Pg
     groups = max(1, min(P, -(-4096 // (T * rows))))
-    Pg = min(-(-P // groups), (2 ** 32 - 1) // max(1, m - 1))
+    Pg = min(-(-P // groups), G.decode_sum_group_limit(m))
     part = torch.empty(-(-P // Pg), rows, L, dtype=torch.int32, device=dev)
+    redo = torch.zeros(1, dtype=torch.int32, device=dev)
     G.decode_sum(rows, P, Pg, L, m, arena.ct, arena.stride, arena.pt_len, pre, tile_sub, part,
-                 out, err)
+                 out, err, redo)
     return out
 
 

@@ -118,6 +118,37 @@ def test_open_sum_matches_torch(cuda, native, L):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("lean", [1, 0])
+@pytest.mark.parametrize("L,m", [(1, 433), (7, 433), (553, 433), (6144, 433), (6145, 433),
+                                 (20000, 433), (40000, 433), (30000, 8191), (9000, 64)])
+def test_open_sum_canonical_streams(cuda, native, L, m, lean):
+    """Canonical shares only (what our participants and any canonical encoder
+    produce): the lean kernel (sums of zigzag codes, k_decode_sum_z) and the
+    generic one (lean switched off) both equal the plain sum. Row kinds stress
+    the range edges: all-1-byte, all-2-byte, alternating and random streams
+    drift apart by up to 2x in bytes, so 1 KiB sub-chunk cuts split varints."""
+    from sda_amd._native import gpu
+
+    def gen(j):
+        kind = j % 5
+        if kind == 0:
+            return [0] * L
+        if kind == 1:
+            return torch.randint(min(64, m - 1), m, (L,)).tolist()
+        if kind == 2:
+            return [(63 + (i & 1)) % m for i in range(L)]
+        if kind == 3:
+            return [(m - 1) if (i % 3) else 1 for i in range(L)]
+        return torch.randint(0, m, (L,)).tolist()
+    gpu().set_decode_lean(lean)
+    try:
+        e, out, ref = _open_sum_case(native, cuda, 2, 11, L, m, gen)
+    finally:
+        gpu().set_decode_lean(1)
+    assert e == 0
+    assert torch.equal(out, ref)
+
+
 def test_open_sum_foreign_encodings(cuda, native):
     """Non-canonical values (>= m, long varints up to 10 bytes) take the generic
     and slow decode paths inside the fused kernel; large modulus (u32 path)."""

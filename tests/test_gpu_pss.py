@@ -73,3 +73,88 @@ def test_pss_shares_uniform(cuda, name):
         chi2 = float(((counts - expected) ** 2 / expected).sum())
         dof = m - 1
         assert chi2 < dof + 6 * (2 * dof) ** 0.5, (c, chi2)
+
+
+# ---- parity with the tss 0.2 FFT construction on the device paths ---------------
+def _fft_model_shares(ps, secrets_rows, seed):
+    """Shares [n][rows] of the FFT construction (tests/helpers.py) for random inputs."""
+    import random
+
+    from helpers import tss_share
+
+    rng = random.Random(seed)
+    p = ps.prime_modulus
+    cols = []
+    for s in secrets_rows:
+        r = [rng.randrange(p) for _ in range(ps.privacy_threshold_)]
+        cols.append(tss_share(list(s), r, ps.privacy_threshold_, ps.share_count, ps.secret_count, p,
+                              ps.omega_secrets, ps.omega_shares))
+    return torch.tensor(cols, dtype=torch.int64).T.contiguous()  # [n][batches]
+
+
+@pytest.mark.parametrize("name", ["483", "4_26_3"])
+def test_fft_model_shares_reconstruct_on_device(cuda, name):
+    """Shares made by the reference's FFT construction (client/src/crypto/sharing/
+    packed_shamir.rs:40-43 -> tss share) reconstruct through the GPU Lagrange
+    kernel (k_pss_reconstruct) and the int8-MFMA GEMM, from every clerk and
+    from dropout subsets (packed_shamir.rs:73-77 -> tss reconstruct)."""
+    import random
+
+    from sda_amd.models import PSS_4_8_3, PSS_4_26_3
+    from sda_amd.ops import gpu as G
+
+    ps = PSS_4_8_3 if name == "483" else PSS_4_26_3
+    nat, p, n, k = ps.native(), ps.prime_modulus, ps.share_count, ps.secret_count
+    B = 257
+    rng = random.Random(11)
+    secrets = [[rng.randrange(p) for _ in range(k)] for _ in range(B)]
+    ys_all = _fft_model_shares(ps, secrets, seed=3)
+    D = B * k - 1  # truncated last batch
+    want = torch.tensor(secrets, dtype=torch.int64).reshape(-1)[:D]
+    need = ps.reconstruction_threshold()
+    for live in (list(range(n)), sorted(rng.sample(range(n), need)),
+                 sorted(rng.sample(range(n), need + 1))):
+        ys = ys_all[live].to(torch.int32).cuda().contiguous()
+        lag = torch.tensor(nat.lagrange_matrix(live), dtype=torch.int64).to(torch.int32).cuda()
+        out = torch.empty(D, dtype=torch.int32, device="cuda")
+        G.pss_reconstruct(ys, lag, k, D, p, out)
+        assert torch.equal(out.cpu().to(torch.int64), want), live
+        kp, limbs = G.padded_k(len(live)), G.limb_count(p)
+        out2 = torch.full((D,), -1, dtype=torch.int32, device="cuda")
+        G.modgemm_i8(G.limbs_of(lag.view(k, len(live)), kp, limbs), G.limbs_t(ys, kp, limbs), p,
+                     out2, ldc_z=0, ldc_m=1, ldc_n=k, limit=D)
+        assert torch.equal(out2.cpu().to(torch.int64), want), live
+
+
+def test_device_shares_are_the_fft_construction(cuda):
+    """The matrix the share kernels apply is the FFT construction: device
+    shares of PSS_4_8_3 interpolate (big-integer Lagrange through {1} u
+    {omega_shares^(i+1)}) to a polynomial of degree <= t + k that is 0 at 1 and
+    holds the secrets at omega_secrets^(1..k)."""
+    from sda_amd.models import PSS_4_8_3
+
+    ps = PSS_4_8_3
+    p, n, k, t = ps.prime_modulus, ps.share_count, ps.secret_count, ps.privacy_threshold_
+    g = torch.Generator(device="cuda").manual_seed(21)
+    secrets = torch.randint(0, p, (2, 3 * 40), dtype=torch.int32, device=cuda, generator=g)
+    _, ys = _shares(cuda, ps, secrets)
+    ys = ys.cpu()
+
+    def interp_at(points, values, x):
+        acc = 0
+        for i, (xi, yi) in enumerate(zip(points, values)):
+            num = den = 1
+            for j, xj in enumerate(points):
+                if j != i:
+                    num, den = num * (x - xj) % p, den * (xi - xj) % p
+            acc = (acc + yi * num * pow(den, p - 2, p)) % p
+        return acc
+
+    pts = [pow(ps.omega_shares, i + 1, p) for i in range(n)]
+    for part in range(2):
+        for b in range(0, 40, 7):
+            vals = [int(ys[c, part, b]) for c in range(n)]
+            # all n = 8 shares lie on one polynomial of degree <= t + k = 7 with f(1) = 0
+            assert interp_at(pts, vals, 1) == 0
+            for e in range(k):
+                assert interp_at(pts, vals, pow(ps.omega_secrets, e + 1, p)) == int(secrets[part, b * k + e])
