@@ -375,7 +375,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
                  uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
                  uint32_t* __restrict__ partials, uint32_t* __restrict__ term_cnt,
                  uint32_t* __restrict__ sub_cnt, int use_mfma) {
-  __shared__ int32_t cpart[2][kWaves][16][kPolyDigits + 1];  // double-buffered per chunk
+  // digit sums of every (chunk of the block, segment): the four waves' K-slices
+  // meet here through LDS adds, and the 130-bit work on them happens once per
+  // block, a lane per segment, instead of per chunk on one wave's 16 lanes
+  __shared__ int32_t cacc[kMacChunksPerBlock][16][kPolyDigits + 1];
   __shared__ uint32_t scratch[kWaves];
   const int j = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -388,10 +391,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   const int k1 = min(K, k0 + kMacChunksPerBlock);
   const bool any_middle = use_mfma && k1 > 1 && k0 < last && max(k0, 1) < min(k1, last);
   // the message's weight-digit fragments (this lane's K-slice of its digit
-  // columns), segment constant and segment factors: loaded once, reused by
-  // every chunk of the block
+  // columns): loaded once, reused by every chunk of the block
   v4i b0[4], b1[4];
-  P130 kseg = p130_zero(), sfac = p130_zero();
   if (any_middle) {
     const int8_t* tab = reinterpret_cast<const int8_t*>(pw + kPowTabOff);
 #pragma unroll
@@ -402,16 +403,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
       if (row < kPolyDigits - 16)
         b1[qq] = *reinterpret_cast<const v4i*>(tab + (16 + row) * kSegBytes + 64 * q + 16 * g);
     }
-    if (wave == 0 && lane < 16) {
-      const uint32_t* pf = pw + (16 * lane + 15) * 5;
-#pragma unroll
-      for (int u = 0; u < 5; ++u) {
-        kseg.v[u] = pw[kPowKsegOff + u];
-        sfac.v[u] = pf[u];
-      }
-    }
+    int32_t* flat = &cacc[0][0][0];
+    for (int i = tid; i < kMacChunksPerBlock * 16 * (kPolyDigits + 1); i += kBlock) flat[i] = 0;
+    __syncthreads();
   }
-  int buf = 0;
   for (int k = k0; k < k1; ++k) {
     const int64_t kC = (int64_t)k * kChunkBytes;
     const int64_t start = kC >= 32 ? kC - 32 : 0;
@@ -449,43 +444,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, b0[qq], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, b1[qq], acc1, 0, 0, 0);
       }
-      // C[segment 4 g + i][digit row]
+      // C[segment 4 g + i][digit row]: |sum| < 2^23 per wave, 2^25 over the four
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        cpart[buf][wave][4 * g + i][row] = acc0[i];
-        if (row < kPolyDigits - 16) cpart[buf][wave][4 * g + i][16 + row] = acc1[i];
+        atomicAdd(&cacc[k - k0][4 * g + i][row], acc0[i]);
+        if (row < kPolyDigits - 16) atomicAdd(&cacc[k - k0][4 * g + i][16 + row], acc1[i]);
       }
-      // all waves' partials are in (and every MAC read of the chunk is done
-      // before its in-place decryption); wave 0 reads this buffer while the
-      // others move on to the next chunk's, and passes the next barrier only
-      // after it is done
-      __syncthreads();
-      if (wave == 0) {
-        P130 h = p130_zero();
-        if (lane < 16) {
-          int32_t c[kPolyDigits];
-#pragma unroll
-          for (int d = 0; d < kPolyDigits; ++d)
-            c[d] = cpart[buf][0][lane][d] + cpart[buf][1][lane][d] + cpart[buf][2][lane][d] +
-                   cpart[buf][3][lane][d];
-          h = p130_mul(poly_seg_value(c, kseg), sfac);
-        }
-        uint64_t d[5];
-#pragma unroll
-        for (int u = 0; u < 5; ++u) d[u] = wave_sum64((uint64_t)h.v[u]);
-        if (lane == 0) {
-          uint64_t cc;
-          cc = d[0] >> 26; d[0] &= kM26; d[1] += cc;
-          cc = d[1] >> 26; d[1] &= kM26; d[2] += cc;
-          cc = d[2] >> 26; d[2] &= kM26; d[3] += cc;
-          cc = d[3] >> 26; d[3] &= kM26; d[4] += cc;
-          cc = d[4] >> 26; d[4] &= kM26; d[0] += cc * 5;
-          cc = d[0] >> 26; d[0] &= kM26; d[1] += cc;
-#pragma unroll
-          for (int u = 0; u < 5; ++u) part[u] = (uint32_t)d[u];
-        }
-      }
-      buf ^= 1;
+      // every MAC read of the chunk is done before its in-place decryption
+      if constexpr (DECRYPT) __syncthreads();
     }
 
     if constexpr (DECRYPT) {
@@ -501,23 +467,31 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
           pt4[u].x ^= w[4 * u]; pt4[u].y ^= w[4 * u + 1]; pt4[u].z ^= w[4 * u + 2]; pt4[u].w ^= w[4 * u + 3];
         }
       }
-      // terminators (MSB clear) among this lane's valid bytes: 64-bit mask + popcount
+      // terminators (MSB clear) among this lane's valid bytes
       const int vlo = (int)max((int64_t)0, start - p0);
       const int vhi = (int)min((int64_t)64, end - p0);
-      uint64_t vmask = 0;
-      if (vhi > vlo) vmask = (vhi >= 64 ? ~0ull : ((1ull << vhi) - 1)) & ~((1ull << vlo) - 1);
-      uint64_t tmask = 0;
+      uint32_t cnt = 0;
+      if (vlo == 0 && vhi == 64) {  // whole lane inside the message: popcounts in place
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t ws[4] = {pt4[q].x, pt4[q].y, pt4[q].z, pt4[q].w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t t = ~ws[u] & 0x80808080u;
-          const uint64_t bits = ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
-          tmask |= bits << (16 * q + 4 * u);
+        for (int q = 0; q < 4; ++q) {
+          cnt += (uint32_t)__popc(~pt4[q].x & 0x80808080u) + (uint32_t)__popc(~pt4[q].y & 0x80808080u) +
+                 (uint32_t)__popc(~pt4[q].z & 0x80808080u) + (uint32_t)__popc(~pt4[q].w & 0x80808080u);
         }
+      } else if (vhi > vlo) {
+        const uint64_t vmask = (vhi >= 64 ? ~0ull : ((1ull << vhi) - 1)) & ~((1ull << vlo) - 1);
+        uint64_t tmask = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t ws[4] = {pt4[q].x, pt4[q].y, pt4[q].z, pt4[q].w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t t = ~ws[u] & 0x80808080u;
+            const uint64_t bits = ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+            tmask |= bits << (16 * q + 4 * u);
+          }
+        }
+        cnt = (uint32_t)__popcll(tmask & vmask);
       }
-      const uint32_t cnt = (uint32_t)__popcll(tmask & vmask);
       if (sub_cnt) {  // per 1 KiB sub-chunk: the 16 lanes covering it
         uint32_t sc = cnt;
 #pragma unroll
@@ -534,6 +508,48 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         const int64_t pos = p0 + 16 * q;
         if (pos >= start - 15 && pos >= 0 && pos < end) *reinterpret_cast<uint4*>(gmsg + pos) = pt4[q];
       }
+    }
+  }
+  if (!any_middle) return;
+  // Segment values -> chunk partials: lane (chunk kk, segment s) turns its 19
+  // digit sums into a 130-bit value and places it by r^(64 (15 - s)); the 16
+  // lanes of a chunk then add up.
+  __syncthreads();
+  if (tid < 16 * kMacChunksPerBlock) {
+    const int kk = tid >> 4, s = tid & 15, k = k0 + kk;
+    const bool mid = k < k1 && k != 0 && k < last;
+    P130 h = p130_zero();
+    if (mid) {
+      int32_t c[kPolyDigits];
+#pragma unroll
+      for (int d = 0; d < kPolyDigits; ++d) c[d] = cacc[kk][s][d];
+      P130 kseg, sfac;
+      const uint32_t* pf = pw + (16 * s + 15) * 5;
+#pragma unroll
+      for (int u = 0; u < 5; ++u) {
+        kseg.v[u] = pw[kPowKsegOff + u];
+        sfac.v[u] = pf[u];
+      }
+      h = p130_mul(poly_seg_value(c, kseg), sfac);
+    }
+    uint64_t d[5];
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      d[u] = h.v[u];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) d[u] += __shfl_xor(d[u], o, 64);
+    }
+    if (mid && s == 0) {
+      uint64_t cc;
+      cc = d[0] >> 26; d[0] &= kM26; d[1] += cc;
+      cc = d[1] >> 26; d[1] &= kM26; d[2] += cc;
+      cc = d[2] >> 26; d[2] &= kM26; d[3] += cc;
+      cc = d[3] >> 26; d[3] &= kM26; d[4] += cc;
+      cc = d[4] >> 26; d[4] &= kM26; d[0] += cc * 5;
+      cc = d[0] >> 26; d[0] &= kM26; d[1] += cc;
+      uint32_t* part = partials + ((size_t)j * K + k) * 8;
+#pragma unroll
+      for (int u = 0; u < 5; ++u) part[u] = (uint32_t)d[u];
     }
   }
 }
