@@ -230,6 +230,12 @@ __global__ void __launch_bounds__(kBlock)
 // lane therefore drops a continuation byte in its last valid position and adds
 // the continuation byte just before its first valid position (from its own
 // words, or from the previous lane's last byte).
+// acc[byte_off / 4] += v on an LDS array (32-bit LDS addressing, no return value)
+SDA_DEV void lds_add(uint32_t* acc, uint32_t byte_off, uint32_t v) {
+  __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(acc) + byte_off), v,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 SDA_DEV uint32_t spread4(uint32_t bits4) {  // 4 bits -> 0xff per set bit, byte k <- bit k
   return ((bits4 * 0x00204081u) & 0x01010101u) * 0xffu;
 }
@@ -263,24 +269,63 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
       info[tid][3] = pt_len[j];
     }
     __syncthreads();
-    for (int i = wave; i < cnt; i += kWaves) {
-      const uint32_t s0 = info[i][0];
-      if (s0 >= (uint32_t)S) continue;  // fewer elements than the tile start: flagged by the totals
-      const uint32_t s1 = min(info[i][1], (uint32_t)S - 1);
-      const int64_t N = info[i][3];
-      const uint8_t* gmsg = pt + ((size_t)r * P + b0 + i) * stride + 48;
-      const int64_t qs = max((int64_t)0, (int64_t)s0 * kSubBytes - 32);
-      const int64_t qe = min(N, ((int64_t)s1 + 1) * kSubBytes - 32);
-      uint32_t rank = info[i][2];
-      for (int64_t c0 = (int64_t)s0 * kSubBytes - 32; c0 < qe; c0 += kWaveBytes) {
+    // This wave's work items of the batch: (message i, 4 KiB pass at c0), walked
+    // as one flat sequence so that the next item's bytes are already in flight
+    // while the current one is processed (an item's loads are otherwise waited
+    // for right after they are issued).
+    int ni = wave;  // next message of the batch to open
+    const uint8_t* n_gmsg = nullptr;
+    int64_t n_c0 = 0, n_qs = 0, n_qe = 0, n_N = 0;
+    uint32_t n_rank = 0;
+    bool n_first = false, n_valid = false;
+    auto open_next = [&]() {  // advance (n_*) to the item after it
+      if (n_valid && n_c0 + kWaveBytes < n_qe) {
+        n_c0 += kWaveBytes;
+        n_first = false;
+        return;
+      }
+      n_valid = false;
+      while (ni < cnt) {
+        const int i = ni;
+        ni += kWaves;
+        const uint32_t s0 = info[i][0];
+        if (s0 >= (uint32_t)S) continue;  // fewer elements than the tile start: flagged by the totals
+        const uint32_t s1 = min(info[i][1], (uint32_t)S - 1);
+        n_N = info[i][3];
+        n_gmsg = pt + ((size_t)r * P + b0 + i) * stride + 48;
+        n_qs = max((int64_t)0, (int64_t)s0 * kSubBytes - 32);
+        n_qe = min(n_N, ((int64_t)s1 + 1) * kSubBytes - 32);
+        n_c0 = (int64_t)s0 * kSubBytes - 32;
+        n_rank = info[i][2];
+        n_first = true;
+        n_valid = n_c0 < n_qe;
+        if (n_valid) return;
+      }
+    };
+    uint32_t wn[16], pn = 0;  // the next item's bytes, and the 4 bytes before lane 0's
+    auto fetch_next = [&]() {
+      const int64_t p0 = n_c0 + 64 * lane;
+      load_lane_bytes(wn, n_gmsg, p0, n_qe);
+      pn = 0;
+      if (lane == 0 && p0 - 4 >= 0 && p0 - 4 < n_N) pn = *reinterpret_cast<const uint32_t*>(n_gmsg + p0 - 4);
+    };
+    open_next();
+    if (n_valid) fetch_next();
+    uint32_t rank = 0;
+    while (n_valid) {
+      const uint8_t* gmsg = n_gmsg;
+      const int64_t c0 = n_c0, qs = n_qs, qe = n_qe, N = n_N;
+      if (n_first) rank = n_rank;
+      uint32_t w[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) w[q] = wn[q];
+      const uint32_t wave_prev = pn;
+      open_next();
+      if (n_valid) fetch_next();
+      {
         const int64_t p0 = c0 + 64 * lane;
-        uint32_t w[16];
-        load_lane_bytes(w, gmsg, p0, qe);
         uint32_t pm1 = __shfl_up(w[15], 1, 64);  // the 4 bytes before this lane's (raw)
-        if (lane == 0) {
-          pm1 = 0;
-          if (p0 - 4 >= 0 && p0 - 4 < N) pm1 = *reinterpret_cast<const uint32_t*>(gmsg + p0 - 4);
-        }
+        if (lane == 0) pm1 = wave_prev;
         const int lo = (int)max((int64_t)0, qs - p0);
         const int hi = (int)min((int64_t)64, qe - p0);
         // a message must end on a terminator
@@ -323,19 +368,35 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         }
         const uint32_t incl = wave_incl_scan(c);
         const uint32_t total = __shfl(incl, 63, 64);
-        uint32_t* a = acc + (rank + kSumMargin - E0 + (incl - c));
-        atomicAdd(a, ((pm1 >> 24) & 0x7fu) & (0u - (pm1 >> 31)));
+        // byte offset (within acc) of the rank of this lane's first terminator
+        uint32_t a4 = 4u * (rank + kSumMargin - E0 + (incl - c));
+        lds_add(acc, a4, ((pm1 >> 24) & 0x7fu) & (0u - (pm1 >> 31)));
         uint32_t wp = pm1;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const uint32_t x = w[q];
-          const uint32_t sh4 = ((__builtin_amdgcn_alignbyte(x, wp, 3) & 0x80808080u) >> 7) * 7u;
-          const uint32_t w7 = x & 0x7f7f7f7fu, tq = tw[q];
+          const uint32_t pc = (__builtin_amdgcn_alignbyte(x, wp, 3) & 0x80808080u) >> 7;
+          // (opaque steps: left to itself the compiler folds these shift-adds into
+          // v_mul_lo_u32, a quarter-rate instruction, and the byte fields below
+          // into bit-field extracts instead of free byte selects)
+          uint32_t sh4 = pc << 3;
+          asm volatile("" : "+v"(sh4));
+          sh4 -= pc;                            // 7 where the previous byte continues, per byte
+          uint32_t w7 = x & 0x7f7f7f7fu;
+          // 4 * (terminators before byte u of this word), per byte
+          uint32_t pre4 = tw[q] >> 5;           // 4 per terminator
+          asm volatile("" : "+v"(pre4));
+          pre4 += pre4 << 8;
+          asm volatile("" : "+v"(pre4));
+          pre4 += pre4 << 16;                   // inclusive
+          asm volatile("" : "+v"(pre4));
+          uint32_t ex4 = pre4 << 8;             // exclusive
+          asm volatile("" : "+v"(ex4), "+v"(w7), "+v"(sh4));
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            atomicAdd(a, ((w7 >> (8 * u)) & 0xffu) << ((sh4 >> (8 * u)) & 0xffu));
-            a += (tq >> (8 * u + 7)) & 1u;
-          }
+          for (int u = 0; u < 4; ++u)
+            lds_add(acc, a4 + ((ex4 >> (8 * u)) & 0xffu),
+                    ((w7 >> (8 * u)) & 0xffu) << ((sh4 >> (8 * u)) & 0xffu));
+          a4 += pre4 >> 24;
           wp = x;
         }
         rank += total;

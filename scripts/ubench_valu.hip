@@ -106,6 +106,36 @@ __global__ void __launch_bounds__(256) k_dsadd(uint32_t* out, int stride, int it
   out[blockIdx.x * 256 + threadIdx.x] = acc[threadIdx.x];
 }
 
+// Scatter shapes of the decode-sum accumulate: every lane walks ranks starting at a
+// pseudo-random base (lanes ~34 ranks apart with data-dependent jitter), MODE 0 =
+// ds_add_u32 on all lanes, 1 = ds_add_u32 with about half the lanes masked off
+// per instruction, 2 = plain ds_write_b32, 3 = ds_add_u32 at consecutive ranks
+// (lane l -> base + l: conflict-free reference).
+template <int MODE>
+__global__ void __launch_bounds__(256) k_scatter(uint32_t* out, int iters, uint32_t seed) {
+  __shared__ uint32_t acc[8192];
+  for (int i = threadIdx.x; i < 8192; i += 256) acc[i] = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t h = (threadIdx.x + 1) * 0x9e3779b9u ^ seed;
+  h ^= h >> 15; h *= 0x85ebca6bu; h ^= h >> 13;
+  uint32_t base = (lane * 34u + (h & 15u)) & 4095u;  // ~34 apart, +-8 jitter
+  if (MODE == 3) base = lane;
+  uint32_t m = h;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const uint32_t idx = (base + (uint32_t)u + (uint32_t)it * 7u) & 8191u;
+      if (MODE == 0 || MODE == 3) atomicAdd(&acc[idx], (uint32_t)u + 1u);
+      if (MODE == 1) { if ((m >> u) & 1u) atomicAdd(&acc[idx], (uint32_t)u + 1u); }
+      if (MODE == 2) acc[idx] = (uint32_t)u + m;
+    }
+    m = m * 1664525u + 1013904223u;
+  }
+  __syncthreads();
+  out[blockIdx.x * 256 + threadIdx.x] = acc[threadIdx.x];
+}
+
 template <typename F>
 float time_ms(F launch) {
   hipEvent_t e0, e1;
@@ -136,6 +166,21 @@ int main() {
       const double adds = (double)blocks * 256 * it2 * 16;
       printf("ds_add_u32 stride %-2d          %8.3f ms  %.3e lane-adds/s  (%.2f wave-inst/cycle/CU at 2.4 GHz)\n",
              stride, m2, adds / (m2 * 1e-3), adds / 64 / (m2 * 1e-3) / 256 / 2.4e9);
+    }
+    {
+      const int it3 = 2048;
+      const char* names[4] = {"ds_add scatter (all lanes)", "ds_add scatter (half lanes)",
+                              "ds_write_b32 scatter", "ds_add consecutive ranks"};
+      float t[4];
+      t[0] = time_ms([&] { hipLaunchKernelGGL(k_scatter<0>, dim3(blocks), dim3(256), 0, 0, out, it3, 1u); });
+      t[1] = time_ms([&] { hipLaunchKernelGGL(k_scatter<1>, dim3(blocks), dim3(256), 0, 0, out, it3, 1u); });
+      t[2] = time_ms([&] { hipLaunchKernelGGL(k_scatter<2>, dim3(blocks), dim3(256), 0, 0, out, it3, 1u); });
+      t[3] = time_ms([&] { hipLaunchKernelGGL(k_scatter<3>, dim3(blocks), dim3(256), 0, 0, out, it3, 1u); });
+      for (int i = 0; i < 4; ++i) {
+        const double winst = (double)blocks * 4 * it3 * 16;
+        printf("%-28s %8.3f ms  %.2f cycles per wave-instruction per CU (2.4 GHz)\n", names[i], t[i],
+               t[i] * 1e-3 * 2.4e9 * 256 / winst);
+      }
     }
     (void)hipFree(out);
   }
