@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Runs the BASELINE.json configs and prints one JSON line each (rank 0).
+"""Runs the benchmark configurations (sda_amd/models/configs.py) and prints one
+JSON line each (rank 0).
 
   --config 1  CLI plumbing: sdad + sda walkthrough, 3 x 10-dim, m=433, additive-3
               (expected reveal 0 2 2 4 4 6 6 8 8 10)
@@ -8,9 +9,13 @@
   --config 4  10k x 125M (GPT-2-small gradient), PSS_4_8_3 (8 clerks), streamed in
               participant waves with accumulator checkpoints
   --config 5  1k x 1M per GPU, packed Shamir 5-of-8 (t=2, k=3) with 3 clerks dropped
+  --config 6  1k x 1M, the reference's PSS_155_728_100 (728 clerks) on the int8-limb
+              MFMA GEMM
+  --config 7  config 5 over a prime below 256 (u8 share storage)
 
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench_configs.py --config 3
-Scaled-down runs: --participants / --dim override the per-rank sizes.
+Scaled-down runs: --participants / --dim override the per-rank sizes;
+--pss-backend valu|mfma forces the packed-Shamir kernel family.
 """
 from __future__ import annotations
 
@@ -22,12 +27,6 @@ import sys
 import tempfile
 import time
 
-# RCCL (one stream per P2P peer) + the engine's side stream need more than the
-# default 4 hardware queues per process, or streams get multiplexed onto one
-# queue and serialise (measured: +6 ms per round). Must precede HIP init.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
@@ -35,7 +34,8 @@ if ROOT not in sys.path:
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 3, 4, 5, 6, 7])
+    ap.add_argument("--pss-backend", default=None, choices=["auto", "valu", "mfma"])
     ap.add_argument("--participants", type=int, default=None, help="per rank")
     ap.add_argument("--dim", type=int, default=None)
     ap.add_argument("--wave", type=int, default=None, help="participants per wave (config 4)")
@@ -105,7 +105,7 @@ def gpu_configs(args):
     import torch.distributed as dist
 
     from sda_amd.engine import DeviceAggregator
-    from sda_amd.models import PSS_4_8_3, Additive, AggregationSpec, pss_5_of_8
+    from sda_amd.models.configs import bench_config
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -113,22 +113,26 @@ def gpu_configs(args):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        import datetime
+
+        dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=600))
     c = args.config
-    m = 433
-    P = args.participants or (10000 // world if c == 4 else 1000)
-    D = args.dim or (125_000_000 if c == 4 else 1_000_000)
-    sharing = {2: Additive(3, m), 3: PSS_4_8_3, 4: PSS_4_8_3, 5: pss_5_of_8(m)}[c]
-    spec = AggregationSpec(D, m, sharing)
-    clerks = [0, 2, 3, 5, 7] if c == 5 else None  # config 5: clerks 1, 4, 6 dropped
+    cfg = bench_config(c)
+    P = args.participants or (cfg.participants // world if cfg.streamed else cfg.participants)
+    D = args.dim or cfg.dimension
+    spec = cfg.spec(D)
+    m = spec.field_modulus
+    clerks = list(cfg.clerks) if cfg.clerks is not None else None
+    backend = args.pss_backend or cfg.pss_backend
 
     if world > 1:
         from sda_amd.parallel import DistributedAggregator
 
-        agg = DistributedAggregator(spec, engine="device", device=dev, layout=args.layout)
+        agg = DistributedAggregator(spec, engine="device", device=dev, layout=args.layout,
+                                    pss_backend=backend)
         eng = agg.engine
     else:
-        agg, eng = None, DeviceAggregator(spec, device=dev)
+        agg, eng = None, DeviceAggregator(spec, device=dev, pss_backend=backend)
 
     def sync():
         torch.cuda.synchronize()
@@ -140,8 +144,8 @@ def gpu_configs(args):
         return torch.randint(0, m, (count, D), dtype=torch.int32, device=dev, generator=g)
 
     ok = None
-    if c == 4:
-        wave = args.wave or 32
+    if cfg.streamed:
+        wave = args.wave or cfg.wave
         ck = (args.checkpoint + f".rank{rank}") if args.checkpoint else None
 
         def make(w, first, count):
@@ -188,12 +192,17 @@ def gpu_configs(args):
             secs = agg.comm.all_reduce_max(secs)
         steps, ms = args.steps, secs / args.steps * 1e3
     if rank == 0:
-        emit({"config": c, "metric": "aggregated secret-shared elements/sec", "unit": "elements/s",
+        emit({"config": c, "name": cfg.name, "what": cfg.what,
+              "metric": "aggregated secret-shared elements/sec", "unit": "elements/s",
               "value": P * world * D / (ms / 1e3), "ms_per_round": ms, "steps": steps,
               "n_gpus": world, "participants": P * world, "dimension": D,
-              "sharing": spec.sharing.to_wire(), "clerks_used": clerks or list(range(spec.n_clerks)),
+              "sharing": spec.sharing.to_wire(),
+              "clerks_used": clerks or f"all {spec.n_clerks}",
+              "pss_backend": ("mfma" if eng._pss_mfma else "valu") if eng._pss is not None else None,
+              "share_storage": str(eng.vdtype).replace("torch.", ""),
               "layout": args.layout if world > 1 else "single GPU",
-              "wave": args.wave or 32 if c == 4 else None, "correct": ok})
+              "hbm_high_water_bytes": torch.cuda.max_memory_allocated(),
+              "wave": (args.wave or cfg.wave) if cfg.streamed else None, "correct": ok})
     if world > 1:
         dist.destroy_process_group()
 

@@ -10,12 +10,25 @@
 // limb products per K-step go into 2L - 1 accumulators by degree d = i + j;
 // the epilogue folds sum_d (acc_d mod p) * (2^(7d) mod p) with Barrett steps.
 //
-// Layouts: A limbs [3][M][Kp] (row-major, k contiguous), B limbs
-// [3][batch][N][Kp] (B stored transposed: each column contiguous in k); Kp is a
+// Layouts: A limbs [L][M][Kp] (row-major, k contiguous), B limbs
+// [L][batch][N][Kp] (B stored transposed: each column contiguous in k); Kp is a
 // multiple of 64 with zero padding. C element (m, n) of batch z is written to
 // C[z*ldc_z + m*ldc_m + n*ldc_n] if that linear index < limit.
-// Tile: 256 threads = 4 waves (2 x 2), each wave 32 x 32 = 2 x 2 MFMA
-// 16x16x64 tiles; workgroup tile 64 x 64.
+//
+// Tiling: a workgroup of 4 waves (2 x 2) owns a 64 (M) x 128 (N) tile of C, a
+// wave 32 x 64 = 2 x 4 MFMA 16x16x64 tiles with 2L - 1 accumulators each. Every
+// K-step's A (64 x 64 B per limb) and B (128 x 64 B per limb) tiles are staged
+// through LDS -- each byte is fetched from L2/HBM once per workgroup instead of
+// once per wave -- in two buffers: the next step's tiles are loaded into
+// registers before the current step's MFMAs and written to the other buffer
+// after them, one barrier per step. Rows are 64 B; a row's four 16-byte chunks
+// are stored XOR-swizzled (chunk ^ {0,2,3,1}[(row >> 2) & 3]) so that the 16
+// lanes ds_read_b128 services together (which mix two chunk indices and three
+// row ranges) hit 16 different 16-byte slots of the 256-byte bank row.
+// K = t + k is short (255 -> 4 steps), so the epilogue matters as much as the
+// MFMAs: with p < 2^21 the 2L - 1 degree sums fold by a 32-bit Horner chain
+// (s <- (s * 2^7 + acc_d) mod p, every intermediate below 2^32) instead of
+// 64-bit multiply-adds.
 #include "device_crypto.hpp"
 #include "kernels.hpp"
 #include "modarith.hpp"
@@ -26,74 +39,142 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int kLimbBits = 7;
+constexpr int kBM = 64, kBN = 128, kBK = 64;
 
-// Fragment of a 16 x 64 int8 operand: lane l holds row (l & 15), k = 16*(l>>4) .. +15.
-SDA_DEV v4i load_frag(const int8_t* base, int row, int rows, int64_t ld, int k0, int lane) {
-  const int r = row + (lane & 15);
-  if (r >= rows) return v4i{0, 0, 0, 0};
-  return *reinterpret_cast<const v4i*>(base + (int64_t)r * ld + k0 + 16 * (lane >> 4));
+SDA_DEV int swz(int row, int chunk) {  // position of a row's 16-byte chunk inside its 64 bytes
+  return chunk ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3);  // {0, 2, 3, 1}
 }
 
 template <typename VT, int kLimbs>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
     k_modgemm_i8(int M, int N, int Kp, ModParams mp, const int8_t* __restrict__ A,
                  const int8_t* __restrict__ B, int64_t b_batch, VT* __restrict__ C,
                  int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int m0 = blockIdx.y * 64 + (wave >> 1) * 32;
-  const int n0 = blockIdx.x * 64 + (wave & 1) * 32;
+  constexpr int kRows = kBM + kBN;                       // staged rows per limb
+  constexpr int kStage = kLimbs * kRows * kBK;           // bytes per buffer
+  constexpr int kDeg = 2 * kLimbs - 1;
+  __shared__ __attribute__((aligned(16))) int8_t lds[2 * kStage];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m_blk = blockIdx.y * kBM, n_blk = blockIdx.x * kBN;
   const int z = blockIdx.z;
   const int64_t a_plane = (int64_t)M * Kp;
   const int8_t* Bz = B + (int64_t)z * (int64_t)N * Kp;
-  const int64_t b_plane = b_batch;  // bytes between limb planes of B
-  v4i acc[2][2][2 * kLimbs - 1];
+
+  // this thread's staging pieces: chunk (tid & 3) of A row tid >> 2 and of B rows
+  // tid >> 2 and 64 + (tid >> 2), for every limb plane: 3 row pointers, 3 LDS offsets
+  static_assert(kBM == 64 && kBN == 128, "staging map assumes a 64 + 128 row stage");
+  const int chunk = tid & 3, srow = tid >> 2;
+  const int8_t* src[3];
+  int dst[3];
+  int64_t plane[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const bool isA = u == 0;
+    const int row = isA ? srow : srow + 64 * (u - 1);
+    const int grow = (isA ? m_blk : n_blk) + row;
+    const bool ok = grow < (isA ? M : N);
+    src[u] = !ok ? nullptr : (isA ? A : Bz) + (int64_t)grow * Kp + 16 * chunk;
+    plane[u] = isA ? a_plane : b_batch;
+    dst[u] = ((isA ? 0 : kBM) + row) * kBK + 16 * swz(row, chunk);
+  }
+  v4i acc[2][4][kDeg];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int d = 0; d < 2 * kLimbs - 1; ++d) acc[i][j][d] = v4i{0, 0, 0, 0};
+      for (int d = 0; d < kDeg; ++d) acc[i][j][d] = v4i{0, 0, 0, 0};
 
-  for (int k0 = 0; k0 < Kp; k0 += 64) {
-    v4i fa[2][kLimbs], fb[2][kLimbs];
+  v4i stage[kLimbs][3];
+  auto fetch = [&](int k0) {
 #pragma unroll
     for (int l = 0; l < kLimbs; ++l)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        fa[i][l] = load_frag(A + l * a_plane, m0 + 16 * i, M, Kp, k0, lane);
-        fb[i][l] = load_frag(Bz + l * b_plane, n0 + 16 * i, N, Kp, k0, lane);
-      }
+      for (int u = 0; u < 3; ++u)
+        stage[l][u] = src[u] ? *reinterpret_cast<const v4i*>(src[u] + l * plane[u] + k0) : v4i{0, 0, 0, 0};
+  };
+  auto commit = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int l = 0; l < kLimbs; ++l)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int u = 0; u < 3; ++u)
+        *reinterpret_cast<v4i*>(lds + buf * kStage + l * kRows * kBK + dst[u]) = stage[l][u];
+  };
+  // fragment addresses: lane l reads row (l & 15) of a 16-row tile, chunk l >> 4
+  const int fr = lane & 15, fg = lane >> 4;
+  const int a_off = (wm * 32 + fr) * kBK + 16 * swz(fr, fg);
+  const int b_off = (kBM + wn * 64 + fr) * kBK + 16 * swz(fr, fg);
+
+  fetch(0);
+  commit(0);
+  __syncthreads();
+  const int nk = Kp / kBK;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int cur = ks & 1;
+    if (ks + 1 < nk) fetch((ks + 1) * kBK);
+    const int8_t* base = lds + cur * kStage;
+    v4i fa[2][kLimbs];
+#pragma unroll
+    for (int l = 0; l < kLimbs; ++l)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        fa[i][l] = *reinterpret_cast<const v4i*>(base + l * kRows * kBK + a_off + 16 * i * kBK);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v4i fb[kLimbs];
+#pragma unroll
+      for (int l = 0; l < kLimbs; ++l)
+        fb[l] = *reinterpret_cast<const v4i*>(base + l * kRows * kBK + b_off + 16 * j * kBK);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int la = 0; la < kLimbs; ++la)
 #pragma unroll
           for (int lb = 0; lb < kLimbs; ++lb)
             acc[i][j][la + lb] =
-                __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i][la], fb[j][lb], acc[i][j][la + lb], 0, 0, 0);
+                __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i][la], fb[lb], acc[i][j][la + lb], 0, 0, 0);
+    }
+    if (ks + 1 < nk) commit(cur ^ 1);
+    __syncthreads();
   }
-  // epilogue: C/D map col = lane & 15, row = 4*(lane >> 4) + r
-  uint32_t w[2 * kLimbs - 1];
+  // epilogue: C/D map col = lane & 15, row = 4*(lane >> 4) + r. Output indices are
+  // built from per-lane bases by additions (the general z/m/n strides would cost
+  // three 64-bit multiplies per element otherwise).
+  uint32_t w[kDeg];
 #pragma unroll
-  for (int d = 0; d < 2 * kLimbs - 1; ++d) w[d] = (uint32_t)(((uint64_t)1 << (kLimbBits * d)) % mp.m);
+  for (int d = 0; d < kDeg; ++d) w[d] = (uint32_t)(((uint64_t)1 << (kLimbBits * d)) % mp.m);
+  const int row0 = m_blk + wm * 32 + 4 * (lane >> 4);
+  const int col0 = n_blk + wn * 64 + (lane & 15);
+  const int64_t base = (int64_t)z * ldc_z + (int64_t)row0 * ldc_m + (int64_t)col0 * ldc_n;
+  const int64_t step_j = 16 * ldc_n, step_i = 16 * ldc_m;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int r = 0; r < 4; ++r) {
+      const int row = row0 + 16 * i + r;
+      if (row >= M) continue;
+      int64_t idx = base + i * step_i + r * ldc_m;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + 16 * i + 4 * (lane >> 4) + r;
-        const int col = n0 + 16 * j + (lane & 15);
-        if (row >= M || col >= N) continue;
-        uint64_t s = 0;
+      for (int j = 0; j < 4; ++j, idx += step_j) {
+        if (col0 + 16 * j >= N) continue;
+        uint32_t out;
+        if constexpr (kLimbs == 3) {
+          // acc_d < 2^31, s < p < 2^21: s * 2^7 + acc_d < 2^32
+          uint32_t s = mod32((uint32_t)acc[i][j][kDeg - 1][r], mp);
 #pragma unroll
-        for (int d = 0; d < 2 * kLimbs - 1; ++d)
-          s += (uint64_t)mod32((uint32_t)acc[i][j][d][r], mp) * w[d];  // < 7 * 2^56
-        const int64_t idx = (int64_t)z * ldc_z + (int64_t)row * ldc_m + (int64_t)col * ldc_n;
-        if (idx < limit) C[idx] = (VT)mod64(s, mp);
+          for (int d = kDeg - 2; d >= 0; --d) s = mod32((s << kLimbBits) + (uint32_t)acc[i][j][d][r], mp);
+          out = s;
+        } else {
+          uint64_t s = 0;
+#pragma unroll
+          for (int d = 0; d < kDeg; ++d)
+            s += (uint64_t)mod32((uint32_t)acc[i][j][d][r], mp) * w[d];  // < 7 * 2^56
+          out = mod64(s, mp);
+        }
+        if (idx < limit) C[idx] = (VT)out;
       }
+    }
 }
 
 template <int kLimbs>
@@ -181,7 +262,7 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
                        int64_t ldc_m, int64_t ldc_n, int64_t limit, hipStream_t s) {
   if (M <= 0 || N <= 0 || batches <= 0) return;
   ModParams mp = make_mod_params(p);
-  dim3 grid((N + 63) / 64, (M + 63) / 64, batches);
+  dim3 grid((N + kBN - 1) / kBN, (M + kBM - 1) / kBM, batches);
 #define SDA_GEMM(VT, L)                                                                      \
   hipLaunchKernelGGL((k_modgemm_i8<VT, L>), grid, dim3(256), 0, s, M, N, Kp, mp, A, B, b_plane, \
                      (VT*)C, ldc_z, ldc_m, ldc_n, limit)

@@ -1,30 +1,77 @@
-"""The five BASELINE.json configurations as named presets."""
+"""The benchmark configurations as named presets (the single table
+`bench_configs.py` runs; numbers 1-5 are BASELINE.json's `configs` list in order).
+
+Each preset: participants per rank, vector dimension, the aggregation spec, the
+clerks that deliver results (None = all; config 5 drops three of eight), whether
+the round is streamed in participant waves, and the packed-Shamir backend.
+"""
 from __future__ import annotations
 
-from .schemes import Additive, AggregationSpec, NoMask, PSS_4_8_3, pss_5_of_8
+from dataclasses import dataclass
+from typing import Callable, Optional, Sequence
+
+from .schemes import (PSS_4_8_3, PSS_155_728_100, Additive, AggregationSpec, NoMask, PackedShamir,
+                      pss_5_of_8)
+
+
+@dataclass(frozen=True)
+class BenchConfig:
+    number: int
+    name: str
+    participants: int              # per rank (config 4: in total, split over the ranks)
+    dimension: int
+    sharing: Callable[[], object]  # () -> sharing scheme (some need the native field helpers)
+    clerks: Optional[Sequence[int]] = None
+    streamed: bool = False
+    wave: int = 32
+    pss_backend: str = "auto"
+    what: str = ""
+
+    def spec(self, dimension: Optional[int] = None) -> AggregationSpec:
+        s = self.sharing()
+        return AggregationSpec(dimension or self.dimension, s.field_modulus, s, NoMask(),
+                               title=self.name)
+
+
+def small_prime_5_of_8(prime: int = 241) -> PackedShamir:
+    """t = 2, k = 3, n = 8 over a prime < 256. The matrix formulation only needs
+    t + k + 1 = 6 distinct secret-side points and n = 8 share points disjoint
+    from them: p = 241 has p - 1 = 240 = 16 * 15, so omega_secrets of order 16
+    and omega_shares of order 15 (coprime orders: the two point sets only share
+    1, which neither uses beyond the fixed zero at 1)."""
+    from .._native import native
+
+    f = native().field
+    g = next(w for w in range(2, prime) if f.mult_order(w, prime) == prime - 1)
+    ws = f.mod_pow(g, (prime - 1) // 16, prime)
+    wn = f.mod_pow(g, (prime - 1) // 15, prime)
+    return PackedShamir(3, 8, 2, prime, ws, wn)
+
 
 BENCH_CONFIGS = {
-    # 1: README CLI example (plumbing)
-    "cli_3x10": dict(participants=3, spec=lambda: AggregationSpec(10, 433, Additive(3, 433))),
-    # 2: headline -- 1k participants x 1M dims, 3-way additive, one MI355X
-    "add3_1kx1m": dict(participants=1000,
-                       spec=lambda: AggregationSpec(1_000_000, 433, Additive(3, 433), NoMask(),
-                                                    title="1k x 1M additive-3")),
-    # 3: packed Shamir k=3 n=8 (PSS_4_8_3)
-    "pss483_1kx1m": dict(participants=1000,
-                         spec=lambda: AggregationSpec(1_000_000, 433, PSS_4_8_3, NoMask(),
-                                                      title="1k x 1M PSS_4_8_3")),
-    # 4: 10k x 125M (GPT-2-small gradient), 8 clerks -- streamed in waves
-    "add8_10kx125m": dict(participants=10_000,
-                          spec=lambda: AggregationSpec(125_000_000, 433, Additive(8, 433),
-                                                       NoMask(), title="10k x 125M additive-8")),
-    # 5: packed Shamir 5-of-8 with clerk dropout
-    "pss5of8_1kx1m": dict(participants=1000,
-                          spec=lambda: AggregationSpec(1_000_000, 433, pss_5_of_8(), NoMask(),
-                                                       title="1k x 1M PSS 5-of-8")),
+    c.number: c for c in [
+        BenchConfig(1, "cli_3x10", 3, 10, lambda: Additive(3, 433),
+                    what="README walkthrough through sdad + sda (CPU plumbing)"),
+        BenchConfig(2, "add3_1kx1m", 1000, 1_000_000, lambda: Additive(3, 433),
+                    what="headline: 1k x 1M, additive-3, one MI355X (= bench.py)"),
+        BenchConfig(3, "pss483_1kx1m", 1000, 1_000_000, lambda: PSS_4_8_3,
+                    what="1k x 1M per GPU, packed Shamir k=3 n=8, committee layout over xGMI"),
+        BenchConfig(4, "pss483_10kx125m", 10_000, 125_000_000, lambda: PSS_4_8_3, streamed=True,
+                    what="10k x 125M (GPT-2-small gradient), 8 clerks, streamed in participant "
+                         "waves with accumulator checkpoints"),
+        BenchConfig(5, "pss5of8_dropout", 1000, 1_000_000, pss_5_of_8, clerks=(0, 2, 3, 5, 7),
+                    what="packed Shamir 5-of-8 (t=2, k=3) with clerks 1, 4, 6 dropped"),
+        BenchConfig(6, "pss155_728_1kx1m", 1000, 1_000_000, lambda: PSS_155_728_100,
+                    pss_backend="mfma",
+                    what="the reference's large parameter set: 728 clerks, k=100, t=155, shares "
+                         "and reconstruction on the int8-limb MFMA GEMM"),
+        BenchConfig(7, "pss5of8_u8_dropout", 1000, 1_000_000, small_prime_5_of_8,
+                    clerks=(0, 2, 3, 5, 7),
+                    what="config 5 over a prime below 256: field elements stored as int8-sized "
+                         "values (u8 shares)"),
+    ]
 }
 
 
-def bench_config(name: str):
-    cfg = BENCH_CONFIGS[name]
-    return cfg["participants"], cfg["spec"]()
+def bench_config(number: int) -> BenchConfig:
+    return BENCH_CONFIGS[number]
