@@ -266,7 +266,9 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
 #define SDA_GEMM(VT, L)                                                                      \
   hipLaunchKernelGGL((k_modgemm_i8<VT, L>), grid, dim3(256), 0, s, M, N, Kp, mp, A, B, b_plane, \
                      (VT*)C, ldc_z, ldc_m, ldc_n, limit)
-  if (value_bytes == 2) {
+  if (value_bytes == 1) {
+    if (limbs == 3) SDA_GEMM(uint8_t, 3); else SDA_GEMM(uint8_t, 4);
+  } else if (value_bytes == 2) {
     if (limbs == 3) SDA_GEMM(uint16_t, 3); else SDA_GEMM(uint16_t, 4);
   } else {
     if (limbs == 3) SDA_GEMM(uint32_t, 3); else SDA_GEMM(uint32_t, 4);

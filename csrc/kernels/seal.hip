@@ -28,7 +28,18 @@ constexpr int kValuesPerLane = kEncodeValues / kBlock;  // 32
 template <typename VT>
 SDA_DEV void load_values(uint32_t (&v)[kValuesPerLane], const VT* src, int e0, int L, bool vec_ok) {
   if (vec_ok && e0 + kValuesPerLane <= L) {
-    if constexpr (sizeof(VT) == 2) {
+    if constexpr (sizeof(VT) == 1) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint4 d = reinterpret_cast<const uint4*>(src + e0)[q];
+        const uint32_t ws[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int b = 0; b < 4; ++b) v[16 * q + 4 * u + b] = (ws[u] >> (8 * b)) & 0xffu;
+        }
+      }
+    } else if constexpr (sizeof(VT) == 2) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint4 d = reinterpret_cast<const uint4*>(src + e0)[q];
@@ -61,7 +72,7 @@ __global__ void __launch_bounds__(kBlock)
     k_encode_encrypt(int L, const VT* __restrict__ vals, const uint32_t* __restrict__ tile_off,
                      const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct, uint64_t stride) {
   // u16 values are at most 3-byte varints, u32 at most 5
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kEncodeValues * (sizeof(VT) == 2 ? 3 : 5) + 128];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kEncodeValues * (sizeof(VT) <= 2 ? 3 : 5) + 128];
   __shared__ uint32_t scratch[kWaves];
   const int t = blockIdx.x, j = blockIdx.y;
   const int T = (L + kTileValues - 1) / kTileValues;  // count tiles per message
@@ -610,7 +621,10 @@ void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
                            uint64_t stride, hipStream_t s) {
   if (M <= 0 || L <= 0) return;
   dim3 grid((L + kEncodeValues - 1) / kEncodeValues, M);
-  if (value_bytes == 2)
+  if (value_bytes == 1)
+    hipLaunchKernelGGL(k_encode_encrypt<uint8_t>, grid, dim3(kBlock), 0, s, L,
+                       (const uint8_t*)vals, tile_off, keys, ct, stride);
+  else if (value_bytes == 2)
     hipLaunchKernelGGL(k_encode_encrypt<uint16_t>, grid, dim3(kBlock), 0, s, L,
                        (const uint16_t*)vals, tile_off, keys, ct, stride);
   else

@@ -829,11 +829,11 @@ __global__ void __launch_bounds__(kBlock)
 constexpr int kPssKS = 3;  // secrets per batch
 constexpr int kPssNC = 8;  // clerks
 
-template <int T>
+template <int T, typename VT>
 __global__ void __launch_bounds__(kBlock)
     k_share_pss48(int P, int D, ModParams mp, uint32_t m3, uint32_t t3,
                   const int32_t* __restrict__ secrets, const uint32_t* __restrict__ mat,
-                  RngKeyArg rng, uint64_t owner_base, uint16_t* __restrict__ shares,
+                  RngKeyArg rng, uint64_t owner_base, VT* __restrict__ shares,
                   uint32_t* __restrict__ cnt) {
   constexpr int K = kPssKS + T;
   constexpr int kPerBlock = 32 / T;      // batches per ChaCha block
@@ -910,7 +910,7 @@ __global__ void __launch_bounds__(kBlock)
       const uint4 m0 = *reinterpret_cast<const uint4*>(&sM[c][0]);
       const uint4 m1 = *reinterpret_cast<const uint4*>(&sM[c][4]);
       const uint32_t row[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
-      uint16_t* out = shares + ((size_t)c * P + p) * B;
+      VT* out = shares + ((size_t)c * P + p) * B;
 #pragma unroll
       for (int g = 0; g < kPerBlock; ++g) {
         uint32_t acc = 0;
@@ -920,7 +920,7 @@ __global__ void __launch_bounds__(kBlock)
         for (int d = 0; d < T; ++d) acc += __umul24(row[kPssKS + d], dg[g * T + d]);
         const uint32_t y = mod32(acc, mp);
         if (ok[g]) {
-          out[bidx[g]] = (uint16_t)y;
+          out[bidx[g]] = (VT)y;
           extra[c] += y >= 64u ? 1u : 0u;
         }
       }
@@ -1079,22 +1079,29 @@ void launch_share_pss(int P, int D, int n, int k, int t, uint32_t p, int value_b
                        owner_base, seeds);
   dim3 grid((B + kTileValues - 1) / kTileValues, P);
   const uint64_t p3 = (uint64_t)p * p * p;
-  if (g_pss48 && value_bytes == 2 && mask_mode == kMaskNone && k == kPssKS && n == kPssNC &&
+  if (g_pss48 && value_bytes <= 2 && mask_mode == kMaskNone && k == kPssKS && n == kPssNC &&
       (t == 2 || t == 4) && p <= 8192u && p3 < (1ull << 32)) {
     const uint32_t t3 = (uint32_t)((1ull << 32) % p3);
-    if (t == 4)
-      hipLaunchKernelGGL(k_share_pss48<4>, grid, dim3(kBlock), 0, s, P, D, mp, (uint32_t)p3, t3,
-                         secrets, share_matrix, rng, owner_base, (uint16_t*)shares, cnt);
-    else
-      hipLaunchKernelGGL(k_share_pss48<2>, grid, dim3(kBlock), 0, s, P, D, mp, (uint32_t)p3, t3,
-                         secrets, share_matrix, rng, owner_base, (uint16_t*)shares, cnt);
+#define SDA_PSS48(TT, VT)                                                                     \
+  hipLaunchKernelGGL((k_share_pss48<TT, VT>), grid, dim3(kBlock), 0, s, P, D, mp, (uint32_t)p3, \
+                     t3, secrets, share_matrix, rng, owner_base, (VT*)shares, cnt)
+    if (value_bytes == 1) {  // p <= 256: a share per byte
+      if (t == 4) SDA_PSS48(4, uint8_t); else SDA_PSS48(2, uint8_t);
+    } else {
+      if (t == 4) SDA_PSS48(4, uint16_t); else SDA_PSS48(2, uint16_t);
+    }
+#undef SDA_PSS48
     return;
   }
 #define SDA_PSS_LAUNCH(VT, MK)                                                             \
   hipLaunchKernelGGL((k_share_pss<VT, MK>), grid, dim3(kBlock), 0, s, P, D, n, k, t, mp,       \
                      small_acc, secrets, share_matrix, rng, owner_base, (VT*)shares, cnt,      \
                      mask_out, mask_cnt, seeds, seed_words, err)
-  if (value_bytes == 2) {
+  if (value_bytes == 1) {
+    if (mask_mode == kMaskFull) SDA_PSS_LAUNCH(uint8_t, kMaskFull);
+    else if (mask_mode == kMaskChaCha) SDA_PSS_LAUNCH(uint8_t, kMaskChaCha);
+    else SDA_PSS_LAUNCH(uint8_t, kMaskNone);
+  } else if (value_bytes == 2) {
     if (mask_mode == kMaskFull) SDA_PSS_LAUNCH(uint16_t, kMaskFull);
     else if (mask_mode == kMaskChaCha) SDA_PSS_LAUNCH(uint16_t, kMaskChaCha);
     else SDA_PSS_LAUNCH(uint16_t, kMaskNone);
@@ -1109,7 +1116,9 @@ void launch_share_pss(int P, int D, int n, int k, int t, uint32_t p, int value_b
 void launch_count(int M, int L, int value_bytes, const void* vals, uint32_t* cnt, hipStream_t s) {
   if (M <= 0 || L <= 0) return;
   dim3 grid((L + kTileValues - 1) / kTileValues, M);
-  if (value_bytes == 2)
+  if (value_bytes == 1)
+    hipLaunchKernelGGL(k_count<uint8_t>, grid, dim3(kBlock), 0, s, L, (const uint8_t*)vals, cnt);
+  else if (value_bytes == 2)
     hipLaunchKernelGGL(k_count<uint16_t>, grid, dim3(kBlock), 0, s, L, (const uint16_t*)vals, cnt);
   else
     hipLaunchKernelGGL(k_count<uint32_t>, grid, dim3(kBlock), 0, s, L, (const uint32_t*)vals, cnt);

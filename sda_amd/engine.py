@@ -136,13 +136,15 @@ class DeviceAggregator:
     """Runs complete aggregation rounds for one :class:`AggregationSpec`."""
 
     def __init__(self, spec: AggregationSpec, device=None, keys: KeyTable | None = None,
-                 time_stages: bool = False, pss_backend: str = "auto"):
+                 time_stages: bool = False, pss_backend: str = "auto", share_storage: str = "auto"):
         self.spec = spec
         self.device = torch.device(device or "cuda")
         self.n = spec.n_clerks
         self.m = spec.field_modulus
         self.keys = keys or KeyTable.generate(self.n + 1, self.device)
         self.vdtype = G.value_dtype(self.m)
+        if isinstance(spec.sharing, PackedShamir) and self.m <= 256 and share_storage != "u16":
+            self.vdtype = torch.uint8  # a field element per byte
         self.time_stages = time_stages
         self._round = 0
         if _KEY_PRIO:

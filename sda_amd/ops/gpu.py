@@ -51,7 +51,10 @@ def value_dtype(modulus: int) -> torch.dtype:
 
 
 def value_bytes(dtype: torch.dtype) -> int:
-    return 2 if dtype == torch.int16 else 4
+    return {torch.uint8: 1, torch.int16: 2}.get(dtype, 4)
+
+
+VALUE_DTYPES = (torch.uint8, torch.int16, torch.int32)
 
 
 def varint_max_len(modulus: int) -> int:
@@ -188,7 +191,9 @@ def share_pss(secrets, n, k, t, prime, matrix, shares, cnt, mask_mode, rng_key, 
     _check(secrets, "secrets", torch.int32)
     _check(matrix, "matrix", torch.int32, numel=n * (k + t))
     vb = value_bytes(shares.dtype)
-    _check(shares, "shares", (torch.int16, torch.int32), numel=n * P * B)
+    _check(shares, "shares", VALUE_DTYPES, numel=n * P * B)
+    if shares.dtype == torch.uint8 and prime > 256:
+        raise ValueError("u8 share storage needs a prime <= 256")
     _check(cnt, "cnt", torch.int32, numel=n * P * tiles(B))
     _check(err, "err", torch.int32, numel=1)
     if mask_mode == MASK_FULL:
@@ -204,7 +209,7 @@ def share_pss(secrets, n, k, t, prime, matrix, shares, cnt, mask_mode, rng_key, 
 
 def count(vals: torch.Tensor, cnt: torch.Tensor):
     M, L = vals.shape
-    _check(vals, "vals", (torch.int16, torch.int32))
+    _check(vals, "vals", VALUE_DTYPES)
     _check(cnt, "cnt", torch.int32, numel=M * tiles(L))
     _gpu().count(M, L, value_bytes(vals.dtype), _ptr(vals), _ptr(cnt), _stream())
 
@@ -226,7 +231,7 @@ def segscan(data: torch.Tensor, totals: torch.Tensor | None):
 
 def encode_encrypt(vals, tile_off, keys, ct, stride):
     M, L = vals.shape
-    _check(vals, "vals", (torch.int16, torch.int32))
+    _check(vals, "vals", VALUE_DTYPES)
     _check(tile_off, "tile_off", torch.int32, numel=M * tiles(L))
     _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
     _check(ct, "ct", torch.uint8, min_numel=M * stride)
@@ -387,6 +392,8 @@ def modgemm_i8(A_limbs: torch.Tensor, B_limbs: torch.Tensor, prime: int, out: to
     if Kb != Kp or Lb != L or L != limb_count(prime):
         raise ValueError("limb shape mismatch")
     vb = value_bytes(out.dtype)
+    if out.dtype == torch.uint8 and prime > 256:
+        raise ValueError("u8 output needs a prime <= 256")
     max_idx = (Z - 1) * ldc_z + (M - 1) * ldc_m + (N - 1) * ldc_n
     if min(limit, max_idx + 1) > out.numel():
         raise ValueError("output too small for the GEMM index map")

@@ -158,3 +158,27 @@ def test_device_shares_are_the_fft_construction(cuda):
             assert interp_at(pts, vals, 1) == 0
             for e in range(k):
                 assert interp_at(pts, vals, pow(ps.omega_secrets, e + 1, p)) == int(secrets[part, b * k + e])
+
+
+# ---- u8 share storage (primes below 256) ------------------------------------------
+@pytest.mark.parametrize("backend", ["valu", "mfma"])
+@pytest.mark.parametrize("storage", ["auto", "u16"])
+def test_round_small_prime_u8_storage(cuda, backend, storage):
+    """5-of-8 packed Shamir over p = 241 with three clerks dropped
+    (protocol/src/crypto.rs:79-155 semantics: any t + k results reconstruct): a
+    field element per byte of share storage, on the register kernel and on the
+    int8-limb MFMA GEMM, against the plain sum -- and the same with u16 storage."""
+    from sda_amd.engine import DeviceAggregator, reference_sum
+    from sda_amd.models import AggregationSpec
+    from sda_amd.models.configs import small_prime_5_of_8
+
+    ps = small_prime_5_of_8()
+    m = ps.prime_modulus
+    spec = AggregationSpec(3 * 5000 + 1, m, ps)
+    agg = DeviceAggregator(spec, cuda, pss_backend=backend, share_storage=storage)
+    assert agg.vdtype == (torch.uint8 if storage == "auto" else torch.int16)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randint(0, m, (7, spec.dimension), dtype=torch.int32, device=cuda, generator=g)
+    for clerks in (None, [0, 2, 3, 5, 7]):
+        res = agg.run_round(x, clerks=clerks)
+        assert torch.equal(res.output, reference_sum(x, m))
