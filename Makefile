@@ -82,7 +82,7 @@ $(GPU_MOD): $(HIP_OBJ) $(BUILD)/hip/gpu_module.o $(CORE_LIB)
 	@mkdir -p $(dir $@)
 	$(HIPCC) -shared --offload-arch=$(GPU_ARCH) -o $@ $^ -pthread
 
-# sanitizer builds of the host control plane (SURVEY 5.2); run the C++ self-test
+# sanitizer builds of the host control plane; run the C++ self-test
 asan: $(BUILD)/asan/sda_selftest
 	$(BUILD)/asan/sda_selftest
 $(BUILD)/asan/sda_selftest: csrc/bin/sda_selftest.cc $(CORE_SRC) $(wildcard csrc/include/sda/*.hpp)

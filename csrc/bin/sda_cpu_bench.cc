@@ -1,4 +1,4 @@
-// Reference-equivalent CPU baseline for the headline metric.
+// Reference-equivalent CPU baseline for the headline metric (aggregated secret-shared elements/s).
 //
 // The reference publishes no numbers and cannot be built here (no Rust), so the
 // comparison point is its algorithm, step for step, in C++ on the host:

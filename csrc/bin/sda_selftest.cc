@@ -3,7 +3,7 @@
 // store backend, the in-process workflow with real client crypto (additive and
 // packed Shamir, with and without masks), and the HTTP server under concurrent
 // REST clients (the multithreaded part the reference ran without any locking
-// analysis; SURVEY 5.2).
+// analysis).
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>

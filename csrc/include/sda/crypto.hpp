@@ -57,7 +57,7 @@ void xsalsa20_xor(uint8_t* out, const uint8_t* in, size_t n, const uint8_t nonce
 // Raw ChaCha20 block with the state words given directly (16 x u32 input).
 void chacha20_block_words(uint32_t out[16], const uint32_t in[16], int rounds = 20);
 
-// rand 0.3 `ChaChaRng`: key = seed words (zero-filled to 8),
+// rand 0.3 `ChaChaRng` (client/src/crypto/masking/chacha.rs:29-39): key = seed words (zero-filled to 8),
 // 128-bit counter in state words 12..15 starting at 0, 20 rounds.
 class ChaChaRng {
  public:

@@ -5,7 +5,7 @@
 // values [0, s_1..s_k, r_1..r_t] at w_s^0..w_s^(t+k) -> inverse radix-2 FFT ->
 // zero-pad -> radix-3 FFT with w_n -> drop point 0; reconstruction by Newton
 // interpolation through {1} U {w_n^(i+1)} evaluated at w_s^1..w_s^k
-// (SURVEY App-C). Both maps are linear, so we express them as matrices:
+// (threshold-secret-sharing 0.2, used at client/src/crypto/sharing/packed_shamir.rs). Both maps are linear, so we express them as matrices:
 //   shares  = M . [s; r]        M: n x (k+t)
 //   secrets = L_I . shares_I    L_I: k x |I|   (any |I| >= t+k: clerk dropout)
 // computed with Lagrange bases, which also covers parameter sets whose point

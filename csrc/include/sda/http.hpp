@@ -1,7 +1,7 @@
 // HTTP/1.1 transport for SDA (reference server-http/src/lib.rs, client-http/src/*).
 //
 // Server: POSIX sockets, an accept thread and a worker pool; routes and status
-// semantics of the reference REST API: JSON bodies, Basic auth
+// semantics of the reference REST API (server-http/src/lib.rs routes): JSON bodies, Basic auth
 // `agent_id:token` with trust-on-first-use at POST /v1/agents/me, 404 +
 // `Resource-not-found: true` for a missing resource, a bare 404 for an unknown
 // route, 401 / 403 / 400 / 500 with a text body for errors.

@@ -9,8 +9,8 @@
 //                  documents with embedded committee / snapshot tags / done flags,
 //                  snapshot transpose as an unwind-group pipeline) on a native
 //                  embedded document engine persisted as JSON files
-// All stores are internally locked (the reference's JFS store had no locking:
-// SURVEY 5.2), so the multithreaded HTTP server is race-free.
+// All stores are internally locked (the reference's JFS store had no locking,
+// server/src/jfs_stores/), so the multithreaded HTTP server is race-free.
 #pragma once
 
 #include <memory>

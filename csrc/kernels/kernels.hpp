@@ -103,7 +103,7 @@ void set_share16(int mode);
 void set_pss48(int mode);
 
 // Packed Shamir: shares = M . [s_1..s_k, r_1..r_t] mod p per batch (M: n x (k+t)
-// host-computed from the tss FFT construction; SURVEY App-C).
+// host-computed from the tss FFT construction).
 void launch_share_pss(int P, int D, int n, int k, int t, uint32_t p, int value_bytes,
                       const int32_t* secrets, const uint32_t* share_matrix, int mask_mode,
                       int seed_words, RngKeyArg rng, uint64_t owner_base, void* shares,

@@ -3,7 +3,7 @@
 // Packed Shamir with the reference's large parameter sets (PSS_155_728_100:
 // K = t + k = 255 inputs, n = 728 shares, p = 746497; PSS_155_19682_100) turns
 // share generation into S = M . X (n x K times K x batches, per participant) and
-// reconstruction into L_I . Y (k x |I| times |I| x batches) -- SURVEY K2/K10.
+// reconstruction into L_I . Y (k x |I| times |I| x batches).
 // Values are split into L = 3 (p < 2^21) or 4 (p < 2^28) 7-bit limbs (int8,
 // non-negative), so every limb product fits the i8 MFMA and a K-sum of up to L
 // limb products per degree stays below 2^31 (K * 127^2 * L < 2^31). The L^2

@@ -4,7 +4,7 @@
 //  * additive sharing  client/src/crypto/sharing/additive.rs:32-51 (n-1 uniform
 //    shares, last = secret - sum), batched per clerk (batched.rs:19-52)
 //  * packed Shamir     client/src/crypto/sharing/packed_shamir.rs:40-43 -> tss
-//    share(); here as the equivalent n x (k+t) matrix product (SURVEY App-C)
+//    share(); here as the equivalent n x (k+t) matrix product
 //  * masks             masking/full.rs:22-34 (uniform mask), masking/chacha.rs:22-53
 //    (rand-0.3 ChaChaRng expansion of a per-participant seed)
 //

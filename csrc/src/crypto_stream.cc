@@ -4,7 +4,7 @@
 // XSalsa20-Poly1305 is the libsodium secretbox used under crypto_box_seal
 // (reference client/src/crypto/encryption/sodium.rs:43,78). ChaChaRng reproduces
 // `rand::ChaChaRng::from_seed` + `gen_range(0, m)` used by the ChaCha mask
-// (client/src/crypto/masking/chacha.rs:29-39,67-72; SURVEY App-D).
+// (client/src/crypto/masking/chacha.rs:29-39,67-72).
 #include <cstring>
 
 #include "sda/crypto.hpp"

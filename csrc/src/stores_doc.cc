@@ -2,7 +2,7 @@
 // backend (server-store-mongodb/src/*.rs), on a native embedded document engine.
 //
 // No MongoDB server or driver exists in this environment, so the engine here
-// implements exactly the operations the reference DAO uses:
+// implements exactly the operations the reference DAO uses (server-store-mongodb/src/*.rs):
 // unique `id` index, find/find_one by dotted-path equality, $set / $push /
 // $pull / $addToSet updates with upsert, update_many, count, and the snapshot
 // transpose pipeline ($match -> $unwind(includeArrayIndex) -> $group -> $sort).
@@ -212,7 +212,7 @@ class DocAgentsStore : public AgentsStore {
     std::vector<ClerkCandidate> out;
     for (auto& d : c_.find({})) {
       const Value* keys = d.find("keys");
-      if (!keys || !keys->is_array() || keys->size() == 0) continue;  // reference bug: SURVEY 7.5
+      if (!keys || !keys->is_array() || keys->size() == 0) continue;  // the reference suggests keyless agents here
       ClerkCandidate c;
       c.id = AgentId::parse(d.at("id").as_string());
       for (auto& e : keys->as_array()) c.keys.push_back(EncryptionKeyId::parse(e.at("id").as_string()));

@@ -255,7 +255,7 @@ class KvAggregationsStore : public AggregationsStore {
   void delete_aggregation(const AggregationId& id) override {
     std::lock_guard<std::mutex> g(mu_);
     aggs_->remove(id.str());
-    committees_->remove(id.str());  // the reference leaves these behind (SURVEY 7.5)
+    committees_->remove(id.str());  // the reference leaves these behind
     auto parts = participations(id);
     for (auto& kv : parts->all()) parts->remove(kv.first);
   }
@@ -358,7 +358,7 @@ class KvClerkingJobsStore : public ClerkingJobsStore {
     return get_as<ClerkingJob>(*f_("jobs/queue/" + clerk.str()), job.str());
   }
   void create_clerking_result(const ClerkingResult& r) override {
-    // atomic queue -> done move (the reference's check-then-write was racy: SURVEY 5.2)
+    // atomic queue -> done move (the reference's check-then-write was racy)
     std::lock_guard<std::mutex> g(mu_);
     auto queue = f_("jobs/queue/" + r.clerk.str());
     auto job = get_as<ClerkingJob>(*queue, r.job.str());

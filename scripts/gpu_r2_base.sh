@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 baseline: bench at the default hardware-queue count and at 16, then the GPU suite.
+# Bench at the default hardware-queue count, at 16 and at 2, then the GPU suite.
 set -e
 mkdir -p gpurun_out
 echo "GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-unset}"

@@ -5,7 +5,7 @@ client}.cc``, bound in ``csrc/python/control_bindings.cc``). Protocol objects
 are plain dicts in the reference's serde JSON wire form (protocol/src/*.rs), so
 what a test builds here is byte-for-byte what crosses the REST API.
 
-Reference seams (SURVEY §1):
+Reference seams:
   * ``Service``           protocol/src/methods.rs  -- the SdaService trait object
   * ``memory_server`` / ``jfs_server``   server/src/lib.rs:34-45
   * ``document_server``   server-store-mongodb/src/lib.rs:64-84 (same data model,

@@ -127,7 +127,7 @@ class PackedShamir:
 
 SharingScheme = Union[Additive, PackedShamir]
 
-# threshold-secret-sharing 0.2 parameter sets
+# threshold-secret-sharing 0.2 parameter sets (protocol/src/crypto.rs PackedShamir fields)
 PSS_4_8_3 = PackedShamir(3, 8, 4, 433, 354, 150)
 PSS_4_26_3 = PackedShamir(3, 26, 4, 433, 354, 17)
 PSS_155_728_100 = PackedShamir(100, 728, 155, 746497, 95660, 610121)

@@ -1,6 +1,6 @@
 """Participant-wave streaming with accumulator checkpoints.
 
-Rounds too large to be resident -- BASELINE config 4 is 10k participants x
+Rounds too large to be resident -- the largest benchmark configuration is 10k participants x
 125M dimensions, i.e. 5 TB of inputs and ~13 TB of packed-Shamir shares -- run
 as waves of W participants through the device engine's participate+clerk
 phase. Only the clerks' running sums (n x B) and the recipient's mask sum (D)

@@ -1,4 +1,4 @@
-"""Stage tracing for the aggregation engines (the reference has none).
+"""Stage tracing for the aggregation engines (the reference has no tracing of its own).
 
 * ``SDA_TRACE=1``: every engine stage boundary (participate / exchange / clerk /
   reduce / reveal / waves) is a roctx marker -- PyTorch's nvtx API is backed by

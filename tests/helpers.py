@@ -81,7 +81,7 @@ def poly1305(msg: bytes, key: bytes) -> bytes:
     return ((acc + s) & ((1 << 128) - 1)).to_bytes(16, "little")
 
 
-# --- tss 0.2 packed Shamir model (FFT construction, SURVEY App-C) ----------
+# --- tss 0.2 packed Shamir model (FFT construction) ----------
 def fft2_inverse(a, omega, p):
     n = len(a)
     inv_omega = pow(omega, p - 2, p)

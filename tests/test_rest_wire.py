@@ -2,7 +2,7 @@
 
 References: server-http/src/lib.rs:131-315 (routes, status mapping, Basic auth,
 `Resource-not-found` header), client-http/src/client.rs:43-102 (status -> result
-mapping), protocol/src/*.rs serde shapes (SURVEY App-A), server/src/jfs_stores/*
+mapping), protocol/src/*.rs serde shapes, server/src/jfs_stores/*
 (directory layout), client-store/src/file.rs (keystore layout).
 """
 import base64

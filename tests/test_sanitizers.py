@@ -1,4 +1,4 @@
-"""Host control plane under AddressSanitizer+UBSan and ThreadSanitizer (SURVEY 5.2).
+"""Host control plane under AddressSanitizer+UBSan and ThreadSanitizer.
 
 Builds csrc/bin/sda_selftest.cc with the sanitizers (make asan / make tsan) and
 runs it: crypto round trips, wire codec, every store backend, full in-process
