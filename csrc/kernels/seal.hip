@@ -442,12 +442,27 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         if (pos >= start - 15 && pos >= 0 && pos < end) pt4[q] = *reinterpret_cast<const uint4*>(gmsg + pos);
       }
     }
-    if (use_mfma && k != 0 && k != last) {
+    const bool middle = use_mfma && k != 0 && k != last;
+    v4i a[4];
+    if (middle) {
       const int64_t lo = kC / 16 - 2 + 64 * row;  // first block of segment `row`
-      v4i a[4];
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq)
         a[qq] = *reinterpret_cast<const v4i*>(gmsg + 16 * (lo + 4 * (4 * wave + qq) + g));
+    }
+    // The keystream needs no loaded byte: computed here, its ~1000 instructions
+    // run while the chunk's loads (issued above) are in flight.
+    uint32_t w[16];
+    bool ks = false;
+    if constexpr (DECRYPT) {
+      const int64_t p0 = 64 * (kC / 64 + tid) - 32;
+      ks = p0 < end && p0 + 64 > start;
+      if (ks) {
+        const MsgKey key = keys[j];
+        salsa20_block(w, key.subkey, key.nonce[0], key.nonce[1], (uint64_t)(kC / 64 + tid));
+      }
+    }
+    if (middle) {
       v4i acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
@@ -466,13 +481,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     }
 
     if constexpr (DECRYPT) {
-      const MsgKey key = keys[j];
       // keystream block b covers message bytes [64b-32, 64b+32)
       const int64_t b = kC / 64 + tid;
       const int64_t p0 = 64 * b - 32;
-      if (p0 < end && p0 + 64 > start) {
-        uint32_t w[16];
-        salsa20_block(w, key.subkey, key.nonce[0], key.nonce[1], (uint64_t)b);
+      if (ks) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           pt4[u].x ^= w[4 * u]; pt4[u].y ^= w[4 * u + 1]; pt4[u].z ^= w[4 * u + 2]; pt4[u].w ^= w[4 * u + 3];

@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Per-kernel resource table of the headline round from rocprofv3 PMC passes.
+
+usage: round_pmc_table.py pmc1.csv pmc2.csv fetch.csv write.csv grbm.csv kernel_stats.csv ROUNDS_IN_STATS
+
+Counters are averaged per dispatch and multiplied by the dispatches per round
+taken from the un-instrumented kernel_stats (PMC runs serialise kernels and
+inflate their durations, so times come from the plain trace).
+
+  lane-ops/B   SQ_INSTS_VALU x 64 lanes / ciphertext bytes of the round
+  valu%        time the kernel would need at the measured integer issue peak
+               (one wave64 VALU instruction per cycle per CU, 2.4 GHz, 256 CUs
+               = 3.9e13 lane-ops/s) over its measured time
+  GHz          GRBM_GUI_ACTIVE / kernel time of the instrumented run: the clock
+               the kernel really ran at (the chip drops below 2.4 GHz under
+               sustained integer load)
+  valu@clk%    valu% recomputed at that clock
+  lds%         SQ_ACTIVE_INST_LDS x 4 / (1024 SIMDs x cycles)
+  conf%        SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS (share of LDS-busy
+               cycles lost to bank conflicts)
+  HBM GB       FETCH_SIZE + WRITE_SIZE, and the bandwidth they imply
+"""
+import csv
+import re
+import sys
+from collections import defaultdict
+
+CLK = 2.4e9
+CUS = 256
+PEAK = CUS * 64 * CLK
+CIPHERTEXT_BYTES = 5.56e9  # 3000 boxes x 1M values x ~1.85 varint bytes
+
+
+def short(name):
+    n = re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", "").replace("sdagpu::", ""))
+    return n.replace("void ", "")[-44:]
+
+
+def load(path):
+    per = defaultdict(lambda: defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        per[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items()}
+
+
+def clocks(path):
+    """GHz per kernel: GRBM_GUI_ACTIVE cycles over the dispatch's own duration."""
+    cyc, ns = defaultdict(float), defaultdict(float)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != "GRBM_GUI_ACTIVE":
+            continue
+        k = short(r["Kernel_Name"])
+        cyc[k] += float(r["Counter_Value"])
+        ns[k] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    return {k: cyc[k] / ns[k] for k in cyc if ns[k] > 0}
+
+
+def main(argv):
+    pm = [load(p) for p in argv[1:5]]
+    gr = clocks(argv[5])
+    argv = argv[:5] + argv[6:]
+    rounds = float(argv[6])
+    stats = {}
+    for r in csv.DictReader(open(argv[5])):
+        stats[short(r["Name"])] = (float(r["Calls"]) / rounds, float(r["TotalDurationNs"]) / 1e6 / rounds)
+    print(f"{'kernel':44s} {'n/rnd':>6s} {'ms/rnd':>7s} {'lane-ops/B':>10s} {'valu%':>6s} {'GHz':>5s} {'v@clk%':>6s} {'lds%':>6s} "
+          f"{'conf%':>6s} {'mfma%':>6s} {'issue%':>6s} {'stall%':>6s} {'wait%':>6s} {'rd GB':>6s} {'wr GB':>6s} {'TB/s':>5s}")
+    tot = defaultdict(float)
+    for k, (calls, ms) in sorted(stats.items(), key=lambda kv: -kv[1][1]):
+        if ms < 0.03:
+            continue
+        a, b, f, w = (p.get(k, {}) for p in pm)
+        valu = a.get("SQ_INSTS_VALU", 0) * calls
+        cyc = ms * 1e-3 * CLK
+        lds = a.get("SQ_ACTIVE_INST_LDS", 0) * calls * 4 / (4 * CUS * cyc)
+        ghz = gr.get(k, 0.0)
+        vclk = valu * 64 / (CUS * 64 * ghz * 1e9) / (ms * 1e-3) if ghz else 0.0
+        conf = a.get("SQ_LDS_BANK_CONFLICT", 0) / max(a.get("SQ_ACTIVE_INST_LDS", 0), 1)
+        mfma = a.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) * calls / (4 * CUS * cyc)
+        wc = max(b.get("SQ_WAVE_CYCLES", 0), 1)
+        rd = f.get("FETCH_SIZE", 0) * calls * 1024 / 1e9
+        wr = w.get("WRITE_SIZE", 0) * calls * 1024 / 1e9
+        print(f"{k:44s} {calls:6.1f} {ms:7.3f} {valu * 64 / CIPHERTEXT_BYTES:10.1f} "
+              f"{100 * valu * 64 / PEAK / (ms * 1e-3):6.1f} {ghz:5.2f} {100 * vclk:6.1f} {100 * lds:6.1f} {100 * conf:6.1f} {100 * mfma:6.1f} "
+              f"{100 * b.get('SQ_ACTIVE_INST_ANY', 0) / wc:6.1f} {100 * b.get('SQ_WAIT_INST_ANY', 0) / wc:6.1f} "
+              f"{100 * b.get('SQ_WAIT_ANY', 0) / wc:6.1f} {rd:6.2f} {wr:6.2f} {(rd + wr) / ms:5.2f}")
+        tot["ms"] += ms
+        tot["valu"] += valu
+        tot["rd"] += rd
+        tot["wr"] += wr
+    print(f"{'sum':44s} {'':6s} {tot['ms']:7.3f} {tot['valu'] * 64 / CIPHERTEXT_BYTES:10.1f} "
+          f"{100 * tot['valu'] * 64 / PEAK / (tot['ms'] * 1e-3):6.1f} {'':54s} {tot['rd']:6.2f} {tot['wr']:6.2f}")
+    print(f"VALU time of the whole round at the issue peak: {tot['valu'] * 64 / PEAK * 1e3:.2f} ms")
+
+
+if __name__ == "__main__":
+    main(sys.argv)
