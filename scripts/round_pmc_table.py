@@ -11,9 +11,9 @@ inflate their durations, so times come from the plain trace).
   valu%        time the kernel would need at the measured integer issue peak
                (one wave64 VALU instruction per cycle per CU, 2.4 GHz, 256 CUs
                = 3.9e13 lane-ops/s) over its measured time
-  GHz          GRBM_GUI_ACTIVE / kernel time of the instrumented run: the clock
-               the kernel really ran at (the chip drops below 2.4 GHz under
-               sustained integer load)
+  GHz          GRBM_GUI_ACTIVE (summed over the 8 XCDs) / 8 / kernel time of the
+               instrumented run: the clock the kernel really ran at (the chip
+               drops below 2.4 GHz under sustained integer load)
   valu@clk%    valu% recomputed at that clock
   lds%         SQ_ACTIVE_INST_LDS x 4 / (1024 SIMDs x cycles)
   conf%        SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS (share of LDS-busy
@@ -27,6 +27,7 @@ from collections import defaultdict
 
 CLK = 2.4e9
 CUS = 256
+XCDS = 8
 PEAK = CUS * 64 * CLK
 CIPHERTEXT_BYTES = 5.56e9  # 3000 boxes x 1M values x ~1.85 varint bytes
 
@@ -52,7 +53,7 @@ def clocks(path):
         k = short(r["Kernel_Name"])
         cyc[k] += float(r["Counter_Value"])
         ns[k] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    return {k: cyc[k] / ns[k] for k in cyc if ns[k] > 0}
+    return {k: cyc[k] / ns[k] / XCDS for k in cyc if ns[k] > 0}
 
 
 def main(argv):
@@ -85,12 +86,14 @@ def main(argv):
               f"{100 * b.get('SQ_ACTIVE_INST_ANY', 0) / wc:6.1f} {100 * b.get('SQ_WAIT_INST_ANY', 0) / wc:6.1f} "
               f"{100 * b.get('SQ_WAIT_ANY', 0) / wc:6.1f} {rd:6.2f} {wr:6.2f} {(rd + wr) / ms:5.2f}")
         tot["ms"] += ms
+        tot["vclk_ms"] += vclk * ms
         tot["valu"] += valu
         tot["rd"] += rd
         tot["wr"] += wr
     print(f"{'sum':44s} {'':6s} {tot['ms']:7.3f} {tot['valu'] * 64 / CIPHERTEXT_BYTES:10.1f} "
           f"{100 * tot['valu'] * 64 / PEAK / (tot['ms'] * 1e-3):6.1f} {'':54s} {tot['rd']:6.2f} {tot['wr']:6.2f}")
-    print(f"VALU time of the whole round at the issue peak: {tot['valu'] * 64 / PEAK * 1e3:.2f} ms")
+    print(f"VALU time of the whole round at the issue peak (2.4 GHz): {tot['valu'] * 64 / PEAK * 1e3:.2f} ms; "
+          f"at the clocks the kernels ran at: {tot['vclk_ms']:.2f} ms")
 
 
 if __name__ == "__main__":
