@@ -361,6 +361,28 @@ SDA_DEV P130 poly_seg_value(const int32_t (&c)[19], const P130& kseg) {
   return p130_carry(p130_add(h, kseg));
 }
 
+// ---- interleaved rows (k_encode_encrypt's MAC; tables: kernels.hpp) ----
+// Row i of the chunk whose first keystream byte is kC takes the blocks jb = i + 16 t.
+// A tile holding the keystream bytes [ks0, ks1) owns the pad bit of the blocks whose
+// first byte (kC + 16 jb) lies in that range: for row i those with t in [T0, T1).
+SDA_DEV void poly_row_owned(int64_t ks0, int64_t ks1, int64_t kC, int i, int& T0, int& T1) {
+  const int64_t d0 = ks0 - kC, d1 = ks1 - kC;
+  const int J0 = d0 <= 0 ? 0 : (int)(((d0 + 15) >> 4) < 1024 ? ((d0 + 15) >> 4) : 1024);
+  const int J1 = d1 <= 0 ? 0 : (int)(((d1 + 15) >> 4) < 1024 ? ((d1 + 15) >> 4) : 1024);
+  T0 = J0 > i ? (J0 - i + 15) >> 4 : 0;
+  T1 = J1 > i ? (J1 - i + 15) >> 4 : 0;
+}
+// Row constant: koff + Q[T1] - Q[T0] (all carried, limbs < 2^26 + small).
+SDA_DEV P130 poly_row_const(const uint32_t* koff, const uint32_t* q0, const uint32_t* q1) {
+  P130 k;
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const uint32_t four_p = 4u * (u == 0 ? kM26 - 4u : kM26);
+    k.v[u] = koff[u] + q1[u] + four_p - q0[u];
+  }
+  return p130_carry(k);
+}
+
 // Final tag = (h mod p + s) mod 2^128, as 4 LE words.
 SDA_DEV void p130_finish(uint32_t (&tag)[4], P130 h, const uint32_t (&s)[4]) {
   uint32_t h0 = h.v[0], h1 = h.v[1], h2 = h.v[2], h3 = h.v[3], h4 = h.v[4], c;

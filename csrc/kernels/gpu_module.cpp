@@ -133,14 +133,22 @@ PYBIND11_MODULE(_sda_gpu, m) {
     check_launch("segscan");
   });
   m.def("encode_encrypt", [](int M, int L, int value_bytes, uintptr_t vals, uintptr_t tile_off,
-                             uintptr_t keys, uintptr_t ct, uint64_t stride, uintptr_t stream) {
+                             uintptr_t keys, uintptr_t ct, uint64_t stride, uintptr_t pows,
+                             uintptr_t pt_len, uintptr_t partials, int K, uintptr_t stream) {
     launch_encode_encrypt(M, L, value_bytes, P<const void>(vals), P<const uint32_t>(tile_off),
-                          P<const MsgKey>(keys), P<uint8_t>(ct), stride, S(stream));
+                          P<const MsgKey>(keys), P<uint8_t>(ct), stride, P<const uint32_t>(pows),
+                          P<const uint32_t>(pt_len), P<uint32_t>(partials), K, S(stream));
     check_launch("encode_encrypt");
   });
-  m.def("poly_powers", [](int M, uintptr_t keys, uintptr_t pows, uintptr_t stream) {
-    launch_poly_powers(M, P<const MsgKey>(keys), P<uint32_t>(pows), S(stream));
+  m.def("poly_powers", [](int M, uintptr_t keys, uintptr_t pows, int interleaved, uintptr_t stream) {
+    launch_poly_powers(M, P<const MsgKey>(keys), P<uint32_t>(pows), interleaved, S(stream));
     check_launch("poly_powers");
+  });
+  m.def("mac_edges", [](int M, int K, uintptr_t keys, uintptr_t pows, uintptr_t ct, uint64_t stride,
+                        uintptr_t pt_len, uintptr_t partials, uintptr_t stream) {
+    launch_mac_edges(M, K, P<const MsgKey>(keys), P<const uint32_t>(pows), P<const uint8_t>(ct), stride,
+                     P<const uint32_t>(pt_len), P<uint32_t>(partials), S(stream));
+    check_launch("mac_edges");
   });
   m.def("mac_chunks", [](int M, int K, uintptr_t keys, uintptr_t pows, uintptr_t ct,
                          uint64_t stride, uintptr_t pt_len, uintptr_t partials, int decrypt,

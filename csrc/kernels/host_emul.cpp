@@ -219,6 +219,132 @@ static void emul_mac_mfma(uint32_t (&tag)[4], const MsgKey& key, const uint8_t* 
   p130_finish(tag, H, s4);
 }
 
+// emulate the seal-side MAC that k_encode_encrypt computes per tile (interleaved
+// rows, tables of k_poly_powers with interleaved != 0), k_mac_horner for the first
+// and last chunk (by the definition of a chunk partial) and k_mac_final. `cuts` are
+// the tile borders (message byte offsets, ascending, first 0, last N).
+static void emul_mac_fused(uint32_t (&tag)[4], const MsgKey& key, const uint8_t* ctbytes, uint32_t N,
+                           const std::vector<uint32_t>& cuts) {
+  const int C = kChunkBytes;
+  const int K = (int)(((int64_t)N + 32 + C - 1) / C);
+  const int last = (int)(((int64_t)N + 31) / C);
+  const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
+  const P130 r = p130_r_from_key(rk);
+  auto carry64 = [](uint64_t (&d)[5]) {
+    uint64_t c;
+    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+    c = d[1] >> 26; d[1] &= kM26; d[2] += c;
+    c = d[2] >> 26; d[2] &= kM26; d[3] += c;
+    c = d[3] >> 26; d[3] &= kM26; d[4] += c;
+    c = d[4] >> 26; d[4] &= kM26; d[0] += c * 5;
+    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+    return P130{{(uint32_t)d[0], (uint32_t)d[1], (uint32_t)d[2], (uint32_t)d[3], (uint32_t)d[4]}};
+  };
+  // ---- tables (k_poly_powers, interleaved)
+  std::vector<uint32_t> pw(kPowWords, 0);
+  P130 r16 = r;
+  for (int q = 0; q < 4; ++q) r16 = p130_mul(r16, r16);
+  std::vector<P130> rp(64);
+  for (int t = 0; t < 64; ++t) rp[t] = p130_carry(p130_pow(r16, (uint32_t)(63 - t)));
+  int8_t* tab = reinterpret_cast<int8_t*>(pw.data() + kPowTabOff);
+  uint64_t sw[5] = {0, 0, 0, 0, 0};
+  for (int pos = 0; pos < kSegBytes; ++pos) {
+    const P130 w = poly_weight(rp[pos / 16], pos % 16);
+    for (int u = 0; u < 5; ++u) sw[u] += w.v[u];
+    for (int d = 0; d < kPolyDigits; ++d) tab[d * kSegBytes + pos] = (int8_t)p130_digit7(w, d);
+  }
+  const P130 koff = poly_kseg(p130_zero(), carry64(sw));
+  for (int u = 0; u < 5; ++u) pw[kPowKsegOff + u] = koff.v[u];
+  for (int i = 0; i < 16; ++i) {
+    const P130 f = p130_carry(p130_pow(r, (uint32_t)(16 - i)));
+    for (int u = 0; u < 5; ++u) pw[kPowRowOff + i * 5 + u] = f.v[u];
+  }
+  for (int T = 0; T <= 64; ++T) {
+    uint64_t d[5] = {0, 0, 0, 0, 0};
+    for (int q = 0; q < T; ++q)
+      for (int u = 0; u < 5; ++u) d[u] += rp[q].v[u];
+    const P130 q128 = p130_carry(p130_mul(carry64(d), p130_bit(128)));
+    for (int u = 0; u < 5; ++u) pw[kPowQOff + T * 5 + u] = q128.v[u];
+  }
+  // ---- tiles
+  std::vector<uint32_t> partials((size_t)K * 8, 0);
+  for (size_t ti = 0; ti + 1 < cuts.size(); ++ti) {
+    const uint32_t a = cuts[ti], tile_bytes = cuts[ti + 1] - cuts[ti];
+    if (tile_bytes == 0) continue;
+    const uint32_t b0 = (32u + a) >> 6, base = 32u + a - 64u * b0;
+    std::vector<uint8_t> lds(base + tile_bytes + 128, 0xEE);  // garbage outside the tile ...
+    std::memcpy(lds.data() + base, ctbytes + a, tile_bytes);
+    const uint32_t v1 = base + tile_bytes;
+    for (uint32_t x = base & ~15u; x < base; ++x) lds[x] = 0;  // ... but the edge blocks are cleared
+    for (uint32_t x = v1; x < ((v1 + 15u) & ~15u); ++x) lds[x] = 0;
+    const int32_t v0a = (int32_t)(base & ~15u), v1a = (int32_t)((v1 + 15u) & ~15u);
+    const uint32_t ks0 = 32u + a, ks1 = ks0 + tile_bytes;
+    const int kf = (int)(ks0 / C), kl = (int)((ks1 - 1u) / C);
+    CHECK(kl - kf < 4, "tile spans too many chunks");
+    for (int k = kf; k <= kl; ++k) {
+      if (k == 0 || k >= last) continue;
+      const int32_t xc = (int32_t)((uint32_t)k * C - 64u * b0);
+      uint64_t dsum[5] = {0, 0, 0, 0, 0};
+      for (int i = 0; i < 16; ++i) {
+        int32_t c[kPolyDigits];
+        for (int d = 0; d < kPolyDigits; ++d) c[d] = 0;
+        for (int t = 0; t < 64; ++t) {
+          const int32_t x = xc + 16 * i + 256 * t;
+          uint8_t piece[16] = {0};
+          if (x >= v0a && x < v1a) std::memcpy(piece, lds.data() + x, 16);
+          for (int b = 0; b < 16; ++b) {
+            const int8_t av = (int8_t)(piece[b] ^ 0x80);
+            for (int d = 0; d < kPolyDigits; ++d) c[d] += (int32_t)av * tab[d * kSegBytes + 16 * t + b];
+          }
+        }
+        int T0, T1;
+        poly_row_owned((int64_t)ks0, (int64_t)ks1, (int64_t)k * C, i, T0, T1);
+        const P130 krow = poly_row_const(pw.data() + kPowKsegOff, pw.data() + kPowQOff + T0 * 5,
+                                         pw.data() + kPowQOff + T1 * 5);
+        const uint32_t* rf = pw.data() + kPowRowOff + i * 5;
+        const P130 h = p130_mul(poly_seg_value(c, krow), P130{{rf[0], rf[1], rf[2], rf[3], rf[4]}});
+        for (int u = 0; u < 5; ++u) dsum[u] += h.v[u];
+      }
+      const P130 part = carry64(dsum);
+      for (int u = 0; u < 5; ++u) partials[(size_t)k * 8 + u] += part.v[u];
+    }
+  }
+  // ---- first and last chunk by definition: sum_i c_i r^(eb - i)
+  for (int k : {0, last}) {
+    if (k == last && last == 0 && k != 0) continue;
+    const int64_t kC = (int64_t)k * C;
+    const int64_t start = kC >= 32 ? kC - 32 : 0;
+    const int64_t end = std::min((int64_t)N, kC + C - 32);
+    P130 h = p130_zero();
+    if (start < end) {
+      std::vector<uint8_t> buf(C + 16, 0);
+      for (int64_t pos = start; pos < end; ++pos) buf[pos - (kC - 32)] = ctbytes[pos];
+      const int64_t fb = start / 16, eb = (end + 15) / 16;
+      for (int64_t i = fb; i < eb; ++i) h = p130_mul(p130_carry(p130_add(h, load_block(buf.data(), i, kC, N))), r);
+    }
+    for (int u = 0; u < 5; ++u) partials[(size_t)k * 8 + u] = h.v[u];
+    if (last == 0) break;
+  }
+  // ---- k_mac_final
+  const P130 rC = p130_pow(r, C / 16);
+  P130 H = p130_zero();
+  int64_t prev = 0;
+  for (int k = 0; k < K; ++k) {
+    const int64_t e = (k < K - 1) ? ((int64_t)(k + 1) * C - 32) / 16 : ((int64_t)N + 15) / 16;
+    const uint32_t* pp = partials.data() + (size_t)k * 8;
+    const P130 hk = P130{{pp[0], pp[1], pp[2], pp[3], pp[4]}};
+    if (k == 0) H = hk;
+    else {
+      const int64_t dd = e - prev;
+      const P130 Rd = (dd == C / 16) ? rC : p130_pow(r, (uint32_t)dd);
+      H = p130_carry(p130_add(p130_mul(H, Rd), hk));
+    }
+    prev = e;
+  }
+  const uint32_t s4[4] = {key.poly_s[0], key.poly_s[1], key.poly_s[2], key.poly_s[3]};
+  p130_finish(tag, H, s4);
+}
+
 int main() {
   // 1. primitives vs host
   for (int it = 0; it < 20; ++it) {
@@ -330,6 +456,38 @@ int main() {
       uint8_t dtb[16];
       bytes(dtb, dt, 4);
       CHECK(std::memcmp(tag, dtb, 16) == 0, "poly1305 mfma random N=%u", N);
+    }
+  }
+  // 6. the encode kernel's per-tile MAC: random tile borders (8 KiB .. 24 KiB tiles,
+  //    as 8192 values of 1..3 bytes give), chunk-aligned and off-by-one borders
+  {
+    uint32_t seedw[2];
+    for (int it = 0; it < 120; ++it) {
+      hc::os_random(reinterpret_cast<uint8_t*>(seedw), 8);
+      uint32_t N = it < 60 ? seedw[0] % 400000u : seedw[0] % 70000u;
+      if (it % 7 == 0) N &= ~15u;
+      if (it % 5 == 0) N = (N / kChunkBytes) * kChunkBytes + (uint32_t)(seedw[0] >> 24) - 40u + 40u * (N < 40u);
+      if (N == 0) N = 1;
+      std::vector<uint8_t> ct(N + 16);
+      if (it % 9 == 0) std::memset(ct.data(), 0xff, ct.size());
+      else hc::os_random(ct.data(), ct.size());
+      std::vector<uint32_t> cuts{0};
+      uint32_t x = seedw[1];
+      while (cuts.back() < N) {
+        x = x * 1664525u + 1013904223u;
+        uint32_t step = 8192u + (x >> 8) % 16385u;
+        if (it % 4 == 1) step = kChunkBytes;                       // borders on the chunk grid
+        if (it % 4 == 2 && cuts.size() == 1) step = kChunkBytes - 32;  // ... on the keystream grid
+        if (it % 4 == 3) step = 8192u + ((x >> 8) % 3u) * 8192u + ((x >> 20) % 3u) - 1u;
+        cuts.push_back(std::min(N, cuts.back() + step));
+      }
+      uint8_t tag[16];
+      hc::poly1305(tag, ct.data(), N, blk0);
+      uint32_t dt[4];
+      emul_mac_fused(dt, mk, ct.data(), N, cuts);
+      uint8_t dtb[16];
+      bytes(dtb, dt, 4);
+      CHECK(std::memcmp(tag, dtb, 16) == 0, "poly1305 fused tiles N=%u it=%d", N, it);
     }
   }
   std::printf(failures ? "host_emul: %d FAILURES\n" : "host_emul: all ok\n", failures);

@@ -25,6 +25,9 @@ typedef int v4i __attribute__((ext_vector_type(4)));  // one i8 MFMA operand fra
 
 constexpr int kValuesPerLane = kEncodeValues / kBlock;  // 32
 
+// Index of a message's last chunk (chunk k covers message bytes [kC - 32, (k+1)C - 32)).
+SDA_DEV int last_chunk(uint32_t N) { return (int)(((int64_t)N + 31) / kChunkBytes); }
+
 template <typename VT>
 SDA_DEV void load_values(uint32_t (&v)[kValuesPerLane], const VT* src, int e0, int L, bool vec_ok) {
   if (vec_ok && e0 + kValuesPerLane <= L) {
@@ -67,13 +70,35 @@ SDA_DEV void load_values(uint32_t (&v)[kValuesPerLane], const VT* src, int e0, i
 // values each into LDS at scanned offsets, every lane then XORs (about) one
 // 64-byte XSalsa20 block in place, and the tile is stored with 16-byte writes
 // (byte writes only at the two tile edges shared with neighbouring tiles).
-template <typename VT>
+//
+// MAC: while the ciphertext is still in LDS the block adds the tile's share of the
+// Poly1305 partials of the message's middle chunks (the first and the last chunk
+// are k_mac_horner's). Poly1305 is linear in the message bytes, so a 16 KiB chunk
+// cut by tile borders is the sum of what each tile sees of it, with the bytes
+// outside the tile read as zero; a block's pad bit 2^128 belongs to the tile that
+// holds the block's first byte. LDS index x is keystream byte 64 b0 + x, i.e. the
+// 16-byte Poly1305 blocks sit on 16-byte LDS boundaries. Rows are interleaved (row
+// i = blocks i, i + 16, ... of the chunk; tables: kernels.hpp), so the 16 lanes of
+// an MFMA operand group read 256 contiguous bytes:
+//   row value  = (sum_pos u_pos W(pos) + row constant + pad bits of the owned blocks)
+//   chunk part = sum_i row value_i * r^(16 - i)     (relative to the chunk's end, as
+//                                                    k_mac_chunks' middle chunks are)
+template <typename VT, bool MAC>
 __global__ void __launch_bounds__(kBlock)
     k_encode_encrypt(int L, const VT* __restrict__ vals, const uint32_t* __restrict__ tile_off,
-                     const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct, uint64_t stride) {
+                     const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct, uint64_t stride,
+                     const uint32_t* __restrict__ pows, const uint32_t* __restrict__ pt_len,
+                     uint32_t* __restrict__ partials, int K) {
   // u16 values are at most 3-byte varints, u32 at most 5
   __shared__ __attribute__((aligned(16))) uint8_t lds[kEncodeValues * (sizeof(VT) <= 2 ? 3 : 5) + 128];
   __shared__ uint32_t scratch[kWaves];
+  // chunks a tile can touch: its bytes span at most 2 + (tile bytes - 2) / chunk bytes
+  constexpr int kSlots = sizeof(VT) <= 2 ? 3 : 4;
+  __shared__ int32_t cacc[MAC ? kSlots : 1][16][kPolyDigits + 1];
+  if constexpr (MAC) {
+    int32_t* flat = &cacc[0][0][0];
+    for (int i = threadIdx.x; i < kSlots * 16 * (kPolyDigits + 1); i += kBlock) flat[i] = 0;
+  }
   const int t = blockIdx.x, j = blockIdx.y;
   const int T = (L + kTileValues - 1) / kTileValues;  // count tiles per message
   const int tid = threadIdx.x;
@@ -132,6 +157,41 @@ __global__ void __launch_bounds__(kBlock)
     }
   }
   __syncthreads();
+  // MAC operands that depend only on the tile's position: requested here, so that
+  // their latency is spent under the keystream computation
+  const int wave = tid >> 6, lane = tid & 63;
+  const int row = lane & 15, g = lane >> 4;
+  const uint32_t ks0 = 32u + a, ks1 = ks0 + tile_bytes;  // the tile's keystream byte range
+  const int kf = (int)(ks0 / kChunkBytes), kl = (int)((ks1 - 1u) / kChunkBytes);
+  int last = 0;
+  bool any = false;
+  v4i wb0[4], wb1[4];
+  P130 krow = p130_zero(), rfac = p130_zero();
+  if constexpr (MAC) {
+    last = last_chunk(pt_len[j]);
+    for (int k = kf; k <= kl; ++k) any = any || (k != 0 && k < last);  // block-uniform
+    if (any) {
+      const uint32_t* pw = pows + (size_t)j * kPowWords;
+      // this wave's K-slice of the message's weight digits (columns `row`, 16 + `row`)
+      const int8_t* tab = reinterpret_cast<const int8_t*>(pw + kPowTabOff);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int q = 4 * wave + qq;
+        wb0[qq] = *reinterpret_cast<const v4i*>(tab + row * kSegBytes + 64 * q + 16 * g);
+        wb1[qq] = v4i{0, 0, 0, 0};
+        if (row < kPolyDigits - 16)
+          wb1[qq] = *reinterpret_cast<const v4i*>(tab + (16 + row) * kSegBytes + 64 * q + 16 * g);
+      }
+      if (wave == 0) {  // lane (slot g, row): constant and factor of its row value
+        const int k = kf + g;
+        int T0, T1;  // the row owns the pad bits of its blocks row + 16 t, t in [T0, T1)
+        poly_row_owned((int64_t)ks0, (int64_t)ks1, (int64_t)k * kChunkBytes, row, T0, T1);
+        krow = poly_row_const(pw + kPowKsegOff, pw + kPowQOff + T0 * 5, pw + kPowQOff + T1 * 5);
+        const uint32_t* rf = pw + kPowRowOff + row * 5;
+        rfac = P130{{rf[0], rf[1], rf[2], rf[3], rf[4]}};
+      }
+    }
+  }
   const MsgKey key = keys[j];
   const uint32_t nblk = (base + tile_bytes + 63) >> 6;
   for (uint32_t blk = tid; blk < nblk; blk += kBlock) {
@@ -144,8 +204,20 @@ __global__ void __launch_bounds__(kBlock)
       d.x ^= w[4 * u]; d.y ^= w[4 * u + 1]; d.z ^= w[4 * u + 2]; d.w ^= w[4 * u + 3];
       q[u] = d;
     }
+    if constexpr (MAC) {
+      // the MAC reads whole 16-byte blocks: clear what the two edge blocks hold of
+      // the neighbouring tiles' positions (same thread as the XOR above, so in order)
+      const uint32_t v1 = base + tile_bytes;
+      if (blk == 0)
+        for (uint32_t x = base & ~15u; x < base; ++x) lds[x] = 0;
+      if (blk == (v1 >> 6))
+        for (uint32_t x = v1; x < ((v1 + 15u) & ~15u); ++x) lds[x] = 0;
+    }
   }
   __syncthreads();
+  // From here the block only drains (stores, MAC): ahead of the waves of other blocks
+  // that are still in their keystream loop, so that its LDS and wave slots free up
+  if constexpr (MAC) __builtin_amdgcn_s_setprio(3);
   uint8_t* gmsg = ct + (size_t)j * stride + 48;
   const uint32_t lo = a & ~15u, hi = (a + tile_bytes + 15u) & ~15u, end = a + tile_bytes;
   for (uint32_t c = lo + 16u * tid; c < hi; c += 16u * kBlock) {
@@ -156,6 +228,65 @@ __global__ void __launch_bounds__(kBlock)
         const uint32_t p = c + q;
         if (p >= a && p < end) gmsg[p] = lds[p - a + base];
       }
+    }
+  }
+  if constexpr (MAC) {
+    if (!any) return;  // block-uniform
+    {
+      const int32_t v0a = (int32_t)(base & ~15u), v1a = (int32_t)((base + tile_bytes + 15u) & ~15u);
+      for (int k = kf; k <= kl; ++k) {
+        if (k == 0 || k >= last) continue;
+        // LDS index of the chunk's first keystream byte (negative: starts before the tile)
+        const int32_t xc = (int32_t)((uint32_t)k * kChunkBytes - 64u * b0);
+        v4i acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int t = 4 * (4 * wave + qq) + g;  // block row + 16 t of the chunk
+          const int32_t x = xc + 16 * row + 256 * t;
+          v4i piece = {0, 0, 0, 0};
+          if (x >= v0a && x < v1a) piece = *reinterpret_cast<const v4i*>(lds + x);
+          piece ^= (int)0x80808080;  // bytes u -> u - 128 (signed)
+          acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(piece, wb0[qq], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(piece, wb1[qq], acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          atomicAdd(&cacc[k - kf][4 * g + i][row], acc0[i]);
+          if (row < kPolyDigits - 16) atomicAdd(&cacc[k - kf][4 * g + i][16 + row], acc1[i]);
+        }
+      }
+    }
+    __syncthreads();
+    // Row values -> chunk part: lane (slot g, row) of the first wave
+    if (wave != 0) return;
+    const int k = kf + g;
+    const bool mid = g < kSlots && k <= kl && k != 0 && k < last && k < K;
+    P130 h = p130_zero();
+    if (mid) {
+      int32_t c[kPolyDigits];
+#pragma unroll
+      for (int d = 0; d < kPolyDigits; ++d) c[d] = cacc[g][row][d];
+      h = p130_mul(poly_seg_value(c, krow), rfac);
+    }
+    uint64_t d[5];
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      d[u] = h.v[u];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) d[u] += __shfl_xor(d[u], o, 64);
+    }
+    if (mid && row == 0) {
+      uint64_t cc;
+      cc = d[0] >> 26; d[0] &= kM26; d[1] += cc;
+      cc = d[1] >> 26; d[1] &= kM26; d[2] += cc;
+      cc = d[2] >> 26; d[2] &= kM26; d[3] += cc;
+      cc = d[3] >> 26; d[3] &= kM26; d[4] += cc;
+      cc = d[4] >> 26; d[4] &= kM26; d[0] += cc * 5;
+      cc = d[0] >> 26; d[0] &= kM26; d[1] += cc;
+      // up to three tiles add to one chunk: limbs stay below 2^28
+      uint32_t* part = partials + ((size_t)j * K + k) * 8;
+#pragma unroll
+      for (int u = 0; u < 5; ++u) atomicAdd(&part[u], (uint32_t)d[u]);
     }
   }
 }
@@ -242,7 +373,8 @@ SDA_DEV P130 block_sum_p130(const P130& h, uint64_t (*red)[kWaves]) {
 //    K_seg of the matrix-core MAC (device_crypto.hpp, poly_seg_value).
 // Depends only on the key: computed once per message on the side stream.
 __global__ void __launch_bounds__(kBlock)
-    k_poly_powers(const MsgKey* __restrict__ keys, uint32_t* __restrict__ pows, int prio) {
+    k_poly_powers(const MsgKey* __restrict__ keys, uint32_t* __restrict__ pows, int prio,
+                  int interleaved) {
   if (prio) __builtin_amdgcn_s_setprio(3);  // side-stream key work (see k_seal_setup)
   __shared__ P130 rp[64];
   __shared__ uint64_t red[5][kWaves];
@@ -258,10 +390,19 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
     for (int u = 0; u < 5; ++u) base[t * 5 + u] = f.v[u];
   }
-  // r^(64 - jb) for the segment's blocks jb = 0..63
+  // r^(64 - jb) for the segment's blocks jb = 0..63; interleaved rows (kernels.hpp):
+  // R^(63 - t) with R = r^16 for the row's blocks i + 16 t
   P130 mine = p130_zero();
   if (t < 64) {
-    mine = p130_carry(p130_pow(r, (uint32_t)(64 - t)));
+    if (interleaved) {
+      P130 r16 = p130_mul(r, r);
+      r16 = p130_mul(r16, r16);
+      r16 = p130_mul(r16, r16);
+      r16 = p130_mul(r16, r16);
+      mine = p130_carry(p130_pow(r16, (uint32_t)(63 - t)));
+    } else {
+      mine = p130_carry(p130_pow(r, (uint32_t)(64 - t)));
+    }
     rp[t] = mine;
   }
   __syncthreads();
@@ -285,16 +426,39 @@ __global__ void __launch_bounds__(kBlock)
   const P130 sw = block_sum_p130(wsum, red);
   const P130 sr = block_sum_p130(mine, red);
   if (t == 0) {
-    const P130 k = poly_kseg(sr, sw);
+    // interleaved: the pad bits are added per row from the prefix table below
+    const P130 k = poly_kseg(interleaved ? p130_zero() : sr, sw);
 #pragma unroll
     for (int u = 0; u < 5; ++u) base[kPowKsegOff + u] = k.v[u];
+  }
+  if (!interleaved) return;
+  if (t < 16) {
+    const P130 f = p130_carry(p130_pow(r, (uint32_t)(16 - t)));
+#pragma unroll
+    for (int u = 0; u < 5; ++u) base[kPowRowOff + t * 5 + u] = f.v[u];
+  }
+  if (t <= 64) {
+    uint64_t d[5] = {0, 0, 0, 0, 0};
+    for (int q = 0; q < t; ++q) {
+#pragma unroll
+      for (int u = 0; u < 5; ++u) d[u] += rp[q].v[u];
+    }
+    uint64_t c;
+    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+    c = d[1] >> 26; d[1] &= kM26; d[2] += c;
+    c = d[2] >> 26; d[2] &= kM26; d[3] += c;
+    c = d[3] >> 26; d[3] &= kM26; d[4] += c;
+    c = d[4] >> 26; d[4] &= kM26; d[0] += c * 5;
+    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+    const P130 sum = P130{{(uint32_t)d[0], (uint32_t)d[1], (uint32_t)d[2], (uint32_t)d[3], (uint32_t)d[4]}};
+    const P130 q128 = p130_carry(p130_mul(sum, p130_bit(128)));
+#pragma unroll
+    for (int u = 0; u < 5; ++u) base[kPowQOff + t * 5 + u] = q128.v[u];
   }
 }
 
 constexpr int kMacChunksPerBlock = 8;  // k_mac_chunks: chunks of one message per block
 
-// Index of a message's last chunk (chunk k covers message bytes [kC - 32, (k+1)C - 32)).
-SDA_DEV int last_chunk(uint32_t N) { return (int)(((int64_t)N + 31) / kChunkBytes); }
 
 // Per-lane Horner Poly1305 partial of chunk k: lane t sums the 4 blocks ending
 // 4 (255 - t) blocks before the chunk end eb (end-aligned, so blocks before the
@@ -628,27 +792,45 @@ void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, hipStream_t 
   hipLaunchKernelGGL(k_segscan, dim3(M), dim3(kBlock), 0, s, T, data, totals);
 }
 
+template <typename VT>
+static void launch_encode_t(dim3 grid, int L, const void* vals, const uint32_t* tile_off,
+                            const MsgKey* keys, uint8_t* ct, uint64_t stride, const uint32_t* pows,
+                            const uint32_t* pt_len, uint32_t* partials, int K, hipStream_t s) {
+  if (pows && pt_len && partials)
+    hipLaunchKernelGGL((k_encode_encrypt<VT, true>), grid, dim3(kBlock), 0, s, L, (const VT*)vals,
+                       tile_off, keys, ct, stride, pows, pt_len, partials, K);
+  else
+    hipLaunchKernelGGL((k_encode_encrypt<VT, false>), grid, dim3(kBlock), 0, s, L, (const VT*)vals,
+                       tile_off, keys, ct, stride, pows, pt_len, partials, K);
+}
+
 void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
                            const uint32_t* tile_off, const MsgKey* keys, uint8_t* ct,
-                           uint64_t stride, hipStream_t s) {
+                           uint64_t stride, const uint32_t* pows, const uint32_t* pt_len,
+                           uint32_t* partials, int K, hipStream_t s) {
   if (M <= 0 || L <= 0) return;
   dim3 grid((L + kEncodeValues - 1) / kEncodeValues, M);
   if (value_bytes == 1)
-    hipLaunchKernelGGL(k_encode_encrypt<uint8_t>, grid, dim3(kBlock), 0, s, L,
-                       (const uint8_t*)vals, tile_off, keys, ct, stride);
+    launch_encode_t<uint8_t>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
   else if (value_bytes == 2)
-    hipLaunchKernelGGL(k_encode_encrypt<uint16_t>, grid, dim3(kBlock), 0, s, L,
-                       (const uint16_t*)vals, tile_off, keys, ct, stride);
+    launch_encode_t<uint16_t>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
   else
-    hipLaunchKernelGGL(k_encode_encrypt<uint32_t>, grid, dim3(kBlock), 0, s, L,
-                       (const uint32_t*)vals, tile_off, keys, ct, stride);
+    launch_encode_t<uint32_t>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
 }
 
 extern int g_powers_prio;  // keys.hip (set_key_prio)
 
-void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s) {
+void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, int interleaved, hipStream_t s) {
   if (M <= 0) return;
-  hipLaunchKernelGGL(k_poly_powers, dim3(M), dim3(kBlock), 0, s, keys, pows, g_powers_prio);
+  hipLaunchKernelGGL(k_poly_powers, dim3(M), dim3(kBlock), 0, s, keys, pows, g_powers_prio,
+                     interleaved);
+}
+
+void launch_mac_edges(int M, int K, const MsgKey* keys, const uint32_t* pows, const uint8_t* ct,
+                      uint64_t stride, const uint32_t* pt_len, uint32_t* partials, hipStream_t s) {
+  if (M <= 0 || K <= 0) return;
+  hipLaunchKernelGGL(k_mac_horner, dim3(2, M), dim3(kBlock), 0, s, K, keys, pows, ct, stride, pt_len,
+                     partials, 0);
 }
 
 static int g_mac_mfma = 1;

@@ -29,7 +29,7 @@ from ._native import native
 from .models.schemes import Additive, AggregationSpec, ChaChaMask, FullMask, PackedShamir
 from .ops import gpu as G
 from .ops.sealed import (Arena, KeySet, open_, open_data, open_setup, open_sum, seal, seal_data,
-                         seal_setup)
+                         seal_encode, seal_mac, seal_setup)
 from .utils.trace import tracing_enabled
 
 _TRACE = tracing_enabled()
@@ -38,6 +38,8 @@ _TRACE = tracing_enabled()
 _OPEN_AFTER_SHARE = os.environ.get("SDA_OPEN_AFTER_SHARE", "1") == "1"
 # "open,powers" wave priorities of the side-stream key kernels (experiments)
 _KEY_PRIO = os.environ.get("SDA_KEY_PRIO")
+# Experimental: the seal-side tag pass per clerk on its own stream (see _participate)
+_MAC_OVERLAP = os.environ.get("SDA_MAC_OVERLAP", "0") == "1"
 
 
 class AggregationError(RuntimeError):
@@ -47,7 +49,7 @@ class AggregationError(RuntimeError):
 _SIDE_STREAMS: dict = {}
 
 
-def concurrent_stream(device, tries: int = 12, spin_us: int = 250) -> "torch.cuda.Stream":
+def concurrent_stream(device, tries: int = 12, spin_us: int = 250, slot: int = 0) -> "torch.cuda.Stream":
     """A stream whose kernels really run beside the current stream's.
 
     HIP multiplexes a process's streams onto few hardware queues (4 by default),
@@ -60,7 +62,7 @@ def concurrent_stream(device, tries: int = 12, spin_us: int = 250) -> "torch.cud
     queue. Falls back to the last candidate (correct, only slower)."""
     dev = torch.device(device)
     main = torch.cuda.current_stream(dev)
-    key = (dev.index, main.cuda_stream)
+    key = (dev.index, main.cuda_stream, slot)
     if key in _SIDE_STREAMS:
         return _SIDE_STREAMS[key]
     gate = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -252,6 +254,12 @@ class DeviceAggregator:
             self._side = concurrent_stream(self.device)
         return self._side
 
+    def _mac_stream(self):
+        if getattr(self, "_macs", None) is None:
+            self._side_stream()
+            self._macs = concurrent_stream(self.device, slot=1)
+        return self._macs
+
     def _live(self, clerks):
         spec, n = self.spec, self.n
         live = list(range(n)) if clerks is None else sorted(set(int(c) for c in clerks))
@@ -389,13 +397,37 @@ class DeviceAggregator:
             if t is not None:
                 t.record_stream(main)
         main.wait_event(ev_sealkeys)
-        seal_data(clerk_arena, ks_clerk, shares.view(n * P, B), err, cnt)
+        ev_mac = None
+        if _MAC_OVERLAP and cnt is not None and len(live) == n:
+            # per clerk: encode on the main stream, the HBM-bound tag pass over the
+            # stored ciphertext on a stream of its own beside the next clerk's encode
+            macs = self._mac_stream()
+            ev_mac = []
+            sh2, cnt2 = shares.view(n * P, B), cnt.view(n * P, -1)
+            for c in range(n):
+                box, kc = clerk_arena.slice(c * P, P), ks_clerk.slice(c * P, P)
+                kc, part = seal_encode(box, kc, sh2[c * P:(c + 1) * P], cnt2[c * P:(c + 1) * P])
+                if c == 0:
+                    self._inject_corruption(clerk_arena)
+                ev = torch.cuda.Event()
+                ev.record(main)
+                with torch.cuda.stream(macs):
+                    macs.wait_event(ev)
+                    seal_mac(box, kc, part, err)
+                    e2 = torch.cuda.Event()
+                    e2.record(macs)
+                    ev_mac.append(e2)
+            clerk_arena.ct.record_stream(macs)
+            clerk_arena.pt_len.record_stream(macs)
+            ks_clerk.record_stream(macs)
+        else:
+            seal_data(clerk_arena, ks_clerk, shares.view(n * P, B), err, cnt)
+            self._inject_corruption(clerk_arena)
         del shares
-        self._inject_corruption(clerk_arena)
         if mask_arena is not None:
             seal_data(mask_arena, ks_mask, mask_vals, err, mask_cnt)
         return {"P": P, "kidx": kidx_clerk, "ev_openkeys": ev_openkeys, "mask_arena": mask_arena,
-                "ko_mask": ko_mask, "inbox": clerk_arena, "ko_clerk": ko_clerk}
+                "ko_mask": ko_mask, "inbox": clerk_arena, "ko_clerk": ko_clerk, "ev_mac": ev_mac}
 
     def _clerk(self, st, live, err):
         """Open + combine an inbox (the local arena or the routed one)."""
@@ -404,7 +436,17 @@ class DeviceAggregator:
         main.wait_event(st["ev_openkeys"])
         inbox = st.pop("inbox")
         ko_clerk = st["ko_clerk"]
-        combined = self._open_combine(inbox, ko_clerk, live, P, err)
+        ev_mac = st.get("ev_mac")
+        if ev_mac is not None:
+            # clerk c's boxes are complete once their tags are written; the last
+            # clerk's tag pass runs beside the first clerk's open
+            combined = torch.empty(len(live), self.spec.batches, dtype=torch.int32, device=self.device)
+            keys = ko_clerk[0] if isinstance(ko_clerk, list) else ko_clerk
+            for c in range(self.n):
+                main.wait_event(ev_mac[c])
+                open_sum(inbox.slice(c * P, P), keys.slice(c * P, P), err, rows=1, out=combined[c])
+        else:
+            combined = self._open_combine(inbox, ko_clerk, live, P, err)
         del inbox
         # recipient's share of the mask work is data-parallel too: open these
         # participants' mask boxes and sum them

@@ -16,7 +16,7 @@ SUB_BYTES = 1024                  # terminator-count granularity of the fused cl
 SUB_PER_CHUNK = CHUNK_BYTES // SUB_BYTES
 SUM_TILE = 6144                   # elements per decode-sum tile (k_decode_sum)
 MSGKEY_BYTES = 80
-POW_WORDS = 6152  # Poly1305 tables per message (k_poly_powers; kernels.hpp kPowWords)
+POW_WORDS = 6560  # Poly1305 tables per message (k_poly_powers; kernels.hpp kPowWords)
 SEAL_OVERHEAD = 48
 
 MASK_NONE, MASK_FULL, MASK_CHACHA = 0, 1, 2
@@ -229,20 +229,47 @@ def segscan(data: torch.Tensor, totals: torch.Tensor | None):
     _gpu().segscan(M, T, _ptr(data), _ptr(totals) if totals is not None else 0, _stream())
 
 
-def encode_encrypt(vals, tile_off, keys, ct, stride):
+def encode_encrypt(vals, tile_off, keys, ct, stride, mac=None):
+    """Varint-encode + encrypt the rows of `vals` into the arena. `mac` =
+    (pows, pt_len, partials, K) fuses the Poly1305 of the middle chunks into the
+    pass: `pows` must be the interleaved tables (``poly_powers(...,
+    interleaved=True)``) and `partials` zeroed; :func:`mac_edges` and
+    :func:`mac_final` complete the tag."""
     M, L = vals.shape
     _check(vals, "vals", VALUE_DTYPES)
     _check(tile_off, "tile_off", torch.int32, numel=M * tiles(L))
     _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
     _check(ct, "ct", torch.uint8, min_numel=M * stride)
+    pows = pt_len = partials = 0
+    K = 0
+    if mac is not None:
+        t_pows, t_len, t_part, K = mac
+        _check(t_pows, "pows", torch.int32, min_numel=M * POW_WORDS)
+        _check(t_len, "pt_len", torch.int32, numel=M)
+        _check(t_part, "partials", torch.int32, numel=M * K * 8)
+        pows, pt_len, partials = _ptr(t_pows), _ptr(t_len), _ptr(t_part)
     _gpu().encode_encrypt(M, L, value_bytes(vals.dtype), _ptr(vals), _ptr(tile_off), _ptr(keys),
-                          _ptr(ct), stride, _stream())
+                          _ptr(ct), stride, pows, pt_len, partials, K, _stream())
 
 
-def poly_powers(M, keys, pows):
+def poly_powers(M, keys, pows, interleaved: bool = False):
+    """Per-message Poly1305 tables; `interleaved` selects the seal-side layout read
+    by the fused MAC of :func:`encode_encrypt` (the chunk factors that
+    `mac_edges` / the Horner kernel read are the same in both)."""
     _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
     _check(pows, "pows", torch.int32, min_numel=M * POW_WORDS)
-    _gpu().poly_powers(M, _ptr(keys), _ptr(pows), _stream())
+    _gpu().poly_powers(M, _ptr(keys), _ptr(pows), 1 if interleaved else 0, _stream())
+
+
+def mac_edges(M, K, keys, pows, ct, stride, pt_len, partials):
+    """Poly1305 partials of every message's first and last chunk (Horner)."""
+    _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
+    _check(pows, "pows", torch.int32, min_numel=M * POW_WORDS)
+    _check(ct, "ct", torch.uint8, min_numel=M * stride)
+    _check(pt_len, "pt_len", torch.int32, numel=M)
+    _check(partials, "partials", torch.int32, numel=M * K * 8)
+    _gpu().mac_edges(M, K, _ptr(keys), _ptr(pows), _ptr(ct), stride, _ptr(pt_len), _ptr(partials),
+                     _stream())
 
 
 def mac_chunks(M, K, keys, pows, ct, stride, pt_len, partials, decrypt, term_cnt=None,

@@ -19,6 +19,7 @@ bytes ``[0, 48 + pt_len[j])`` are a wire-format `Encryption` blob.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -86,25 +87,31 @@ class Arena:
 @dataclass
 class KeySet:
     """Per-message derived keys: the 80-byte `MsgKey` records (XSalsa20 subkey,
-    nonce tail, Poly1305 r/s) and each message's Poly1305 chunk-factor table
-    r^(4(255-t)), t < 256 (5 x 26-bit limbs), which lets `k_mac_chunks` combine
-    a 16 KiB chunk with one multiply per lane. Both depend only on the key
-    agreement, so they are produced together on the side stream."""
+    nonce tail, Poly1305 r/s) and each message's Poly1305 tables (chunk factors
+    r^(4(255-t)) plus the weight digits of the matrix-core MAC). Both depend only
+    on the key agreement, so they are produced together on the side stream.
+
+    `sealing` key sets get the interleaved-row tables that the fused MAC of the
+    encode kernel reads (unless that fusion is switched off); opening ones the
+    contiguous-segment tables of `k_mac_chunks`."""
     M: int
     keys: torch.Tensor  # uint8 [M * MSGKEY_BYTES]
     pows: torch.Tensor | None  # int32 [M * POW_WORDS]; None = not derived yet
+    sealing: bool = False
+    interleaved: bool = False  # layout of `pows`
 
     @classmethod
     def derive(cls, M: int, keys: torch.Tensor) -> "KeySet":
         return cls(M, keys, None).with_powers()
 
     def with_powers(self) -> "KeySet":
-        """The chunk-factor table (on the current stream) if not derived yet."""
+        """The Poly1305 tables (on the current stream) if not derived yet."""
         if self.pows is not None:
             return self
         pows = torch.empty(self.M * G.POW_WORDS, dtype=torch.int32, device=self.keys.device)
-        G.poly_powers(self.M, self.keys, pows)
-        return KeySet(self.M, self.keys, pows)
+        il = self.sealing and FUSED_SEAL_MAC
+        G.poly_powers(self.M, self.keys, pows, interleaved=il)
+        return KeySet(self.M, self.keys, pows, self.sealing, il)
 
     def slice(self, first: int, count: int) -> "KeySet":
         """Keys of messages [first, first+count) (no copy)."""
@@ -112,12 +119,18 @@ class KeySet:
             raise ValueError("key slice out of range")
         kb, pw = G.MSGKEY_BYTES, G.POW_WORDS
         return KeySet(count, self.keys[first * kb:(first + count) * kb],
-                      None if self.pows is None else self.pows[first * pw:(first + count) * pw])
+                      None if self.pows is None else self.pows[first * pw:(first + count) * pw],
+                      self.sealing, self.interleaved)
 
     def record_stream(self, stream) -> None:
         self.keys.record_stream(stream)
         if self.pows is not None:
             self.pows.record_stream(stream)
+
+
+# The seal-side Poly1305 inside the encode kernel (default). False = a separate
+# MAC pass over the stored ciphertext (k_mac_chunks<0>) -- A/B measurements.
+FUSED_SEAL_MAC = os.environ.get("SDA_FUSED_SEAL_MAC", "0") == "1"
 
 
 def seal_setup(arena: Arena, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: bytes,
@@ -134,12 +147,14 @@ def seal_setup(arena: Arena, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: 
     keys = torch.empty(arena.M * G.MSGKEY_BYTES, dtype=torch.uint8, device=arena.ct.device)
     G.seal_setup(arena.M, rng_key, owner_base, key_idx, pks, arena.ct, arena.stride, keys, err,
                  gate=gate)
-    return KeySet(arena.M, keys, None)
+    return KeySet(arena.M, keys, None, sealing=True)
 
 
-def seal_data(arena: Arena, keys: KeySet, values: torch.Tensor, err: torch.Tensor,
-              cnt: torch.Tensor | None = None) -> Arena:
-    """Varint-encode + encrypt + MAC the rows of `values` [M][L] into `arena`."""
+def seal_encode(arena: Arena, keys: KeySet, values: torch.Tensor,
+                cnt: torch.Tensor | None = None):
+    """First half of :func:`seal_data`: varint-encode + encrypt the rows of
+    `values` [M][L] into `arena` (ciphertext and lengths; no tag yet). Returns
+    what :func:`seal_mac` needs."""
     M, L = values.shape
     if M != arena.M or L != arena.L:
         raise ValueError("values do not match the arena shape")
@@ -153,14 +168,40 @@ def seal_data(arena: Arena, keys: KeySet, values: torch.Tensor, err: torch.Tenso
     if keys.M != M:
         raise ValueError("key set does not match the arena")
     G.segscan(cnt, arena.pt_len)  # cnt becomes the tile byte offsets
-    G.encode_encrypt(values, cnt, keys.keys, arena.ct, arena.stride)
     keys = keys.with_powers()
-    partials = torch.empty(M * arena.K * 8, dtype=torch.int32, device=dev)
-    G.mac_chunks(M, arena.K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
-                 decrypt=False)
+    partials = None
+    if keys.interleaved:
+        # one pass: every tile adds its share of the middle chunks' Poly1305 partials
+        # while its ciphertext is in LDS; the first / last chunks follow by Horner
+        partials = torch.zeros(M * arena.K * 8, dtype=torch.int32, device=dev)
+        G.encode_encrypt(values, cnt, keys.keys, arena.ct, arena.stride,
+                         mac=(keys.pows, arena.pt_len, partials, arena.K))
+    else:
+        G.encode_encrypt(values, cnt, keys.keys, arena.ct, arena.stride)
+    return keys, partials
+
+
+def seal_mac(arena: Arena, keys: KeySet, partials, err: torch.Tensor) -> Arena:
+    """Second half of :func:`seal_data`: the Poly1305 tag of every box into its
+    header. Reads the stored ciphertext (all of it, or only the first and last
+    chunk of every message when the encode pass already did the middle ones)."""
+    M, dev = arena.M, arena.ct.device
+    if keys.interleaved:
+        G.mac_edges(M, arena.K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials)
+    else:
+        partials = torch.empty(M * arena.K * 8, dtype=torch.int32, device=dev)
+        G.mac_chunks(M, arena.K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
+                     decrypt=False)
     G.mac_final(M, arena.K, keys.keys, arena.ct, arena.stride, arena.pt_len, partials, verify=False,
                 err=err)
     return arena
+
+
+def seal_data(arena: Arena, keys: KeySet, values: torch.Tensor, err: torch.Tensor,
+              cnt: torch.Tensor | None = None) -> Arena:
+    """Varint-encode + encrypt + MAC the rows of `values` [M][L] into `arena`."""
+    keys, partials = seal_encode(arena, keys, values, cnt)
+    return seal_mac(arena, keys, partials, err)
 
 
 def seal(values: torch.Tensor, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: bytes,
