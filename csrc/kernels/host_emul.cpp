@@ -127,123 +127,28 @@ static void emul_mac(uint32_t (&tag)[4], const MsgKey& key, const uint8_t* ctbyt
   p130_finish(tag, H, s4);
 }
 
-// emulate k_poly_powers tables + the matrix-core k_mac_chunks<0> + k_mac_final
-// (the MFMA is an explicit integer dot product; the irregular-segment lanes run
-// the same Horner code as the device)
-static void emul_mac_mfma(uint32_t (&tag)[4], const MsgKey& key, const uint8_t* ctbytes, uint32_t N) {
-  const int C = kChunkBytes;
-  const int K = (int)(((int64_t)N + 32 + C - 1) / C);
-  const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
-  const P130 r = p130_r_from_key(rk);
-  // tables
-  std::vector<P130> fac(256);
-  P130 r4 = p130_mul(r, r);
-  r4 = p130_mul(r4, r4);
-  for (int t = 0; t < 256; ++t) fac[t] = p130_carry(p130_pow(r4, (uint32_t)(255 - t)));
-  std::vector<P130> rp(64);
-  for (int t = 0; t < 64; ++t) rp[t] = p130_carry(p130_pow(r, (uint32_t)(64 - t)));
-  std::vector<int8_t> tab(kPolyDigits * kSegBytes);
-  uint64_t sw[5] = {0, 0, 0, 0, 0}, sr[5] = {0, 0, 0, 0, 0};
-  for (int pos = 0; pos < kSegBytes; ++pos) {
-    const P130 w = poly_weight(rp[pos / 16], pos % 16);
-    for (int u = 0; u < 5; ++u) sw[u] += w.v[u];
-    for (int d = 0; d < kPolyDigits; ++d) tab[d * kSegBytes + pos] = (int8_t)p130_digit7(w, d);
-  }
-  for (int t = 0; t < 64; ++t)
-    for (int u = 0; u < 5; ++u) sr[u] += rp[t].v[u];
-  auto carry64 = [](uint64_t (&d)[5]) {
-    uint64_t c;
-    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
-    c = d[1] >> 26; d[1] &= kM26; d[2] += c;
-    c = d[2] >> 26; d[2] &= kM26; d[3] += c;
-    c = d[3] >> 26; d[3] &= kM26; d[4] += c;
-    c = d[4] >> 26; d[4] &= kM26; d[0] += c * 5;
-    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
-    return P130{{(uint32_t)d[0], (uint32_t)d[1], (uint32_t)d[2], (uint32_t)d[3], (uint32_t)d[4]}};
-  };
-  const P130 kseg = poly_kseg(carry64(sr), carry64(sw));
-  std::vector<P130> parts(K);
-  for (int k = 0; k < K; ++k) {
-    std::vector<uint8_t> buf(C, 0xAA);
-    const int64_t kC = (int64_t)k * C;
-    const int64_t start = kC >= 32 ? kC - 32 : 0;
-    const int64_t end = std::min((int64_t)N, kC + C - 32);
-    if (start >= end) { parts[k] = p130_zero(); continue; }
-    for (int64_t pos = start; pos < end; ++pos) buf[pos - (kC - 32)] = ctbytes[pos];
-    const int64_t fb = start / 16, eb = (end + 15) / 16, nfull = N / 16;
-    uint64_t d[5] = {0, 0, 0, 0, 0};
-    for (int s = 0; s < 16; ++s) {
-      const int64_t lo = eb - 64 * (int64_t)(16 - s);
-      if (lo >= fb && lo + 64 <= nfull) {  // regular: "MFMA" row
-        int32_t c[kPolyDigits];
-        for (int dd = 0; dd < kPolyDigits; ++dd) {
-          int32_t acc = 0;
-          for (int pos = 0; pos < kSegBytes; ++pos) {
-            const int8_t a = (int8_t)(buf[32 + 16 * lo - kC + pos] ^ 0x80);
-            acc += (int32_t)a * tab[dd * kSegBytes + pos];
-          }
-          c[dd] = acc;
-        }
-        const P130 h = p130_mul(poly_seg_value(c, kseg), fac[16 * s + 15]);
-        for (int u = 0; u < 5; ++u) d[u] += h.v[u];
-      } else if (lo + 64 > fb) {  // irregular: lanes 16 s .. 16 s + 15
-        for (int tid = 16 * s; tid < 16 * s + 16; ++tid) {
-          P130 hh = p130_zero();
-          for (int q = 0; q < 4; ++q) {
-            const int64_t i = eb - 4 * (int64_t)(256 - tid) + q;
-            P130 cb = p130_zero();
-            if (i >= fb) cb = load_block(buf.data(), i, kC, N);
-            hh = p130_mul(p130_add(hh, cb), r);
-          }
-          hh = p130_mul(hh, fac[tid]);
-          for (int u = 0; u < 5; ++u) d[u] += hh.v[u];
-        }
-      }
-    }
-    parts[k] = carry64(d);
-  }
-  const P130 rC = p130_pow(r, C / 16);
-  P130 H = p130_zero();
-  int64_t prev = 0;
-  for (int k = 0; k < K; ++k) {
-    const int64_t e = (k < K - 1) ? ((int64_t)(k + 1) * C - 32) / 16 : ((int64_t)N + 15) / 16;
-    if (k == 0) H = parts[k];
-    else {
-      const int64_t dd = e - prev;
-      const P130 Rd = (dd == C / 16) ? rC : p130_pow(r, (uint32_t)dd);
-      H = p130_carry(p130_add(p130_mul(H, Rd), parts[k]));
-    }
-    prev = e;
-  }
-  const uint32_t s4[4] = {key.poly_s[0], key.poly_s[1], key.poly_s[2], key.poly_s[3]};
-  p130_finish(tag, H, s4);
+static P130 carry64(uint64_t (&d)[5]) {
+  uint64_t c;
+  c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+  c = d[1] >> 26; d[1] &= kM26; d[2] += c;
+  c = d[2] >> 26; d[2] &= kM26; d[3] += c;
+  c = d[3] >> 26; d[3] &= kM26; d[4] += c;
+  c = d[4] >> 26; d[4] &= kM26; d[0] += c * 5;
+  c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+  return P130{{(uint32_t)d[0], (uint32_t)d[1], (uint32_t)d[2], (uint32_t)d[3], (uint32_t)d[4]}};
 }
 
-// emulate the seal-side MAC that k_encode_encrypt computes per tile (interleaved
-// rows, tables of k_poly_powers with interleaved != 0), k_mac_horner for the first
-// and last chunk (by the definition of a chunk partial) and k_mac_final. `cuts` are
-// the tile borders (message byte offsets, ascending, first 0, last N).
-static void emul_mac_fused(uint32_t (&tag)[4], const MsgKey& key, const uint8_t* ctbytes, uint32_t N,
-                           const std::vector<uint32_t>& cuts) {
-  const int C = kChunkBytes;
-  const int K = (int)(((int64_t)N + 32 + C - 1) / C);
-  const int last = (int)(((int64_t)N + 31) / C);
-  const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
-  const P130 r = p130_r_from_key(rk);
-  auto carry64 = [](uint64_t (&d)[5]) {
-    uint64_t c;
-    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
-    c = d[1] >> 26; d[1] &= kM26; d[2] += c;
-    c = d[2] >> 26; d[2] &= kM26; d[3] += c;
-    c = d[3] >> 26; d[3] &= kM26; d[4] += c;
-    c = d[4] >> 26; d[4] &= kM26; d[0] += c * 5;
-    c = d[0] >> 26; d[0] &= kM26; d[1] += c;
-    return P130{{(uint32_t)d[0], (uint32_t)d[1], (uint32_t)d[2], (uint32_t)d[3], (uint32_t)d[4]}};
-  };
-  // ---- tables (k_poly_powers, interleaved)
+// the tables of k_poly_powers (layout: kernels.hpp)
+static std::vector<uint32_t> emul_tables(const P130& r) {
   std::vector<uint32_t> pw(kPowWords, 0);
-  P130 r16 = r;
-  for (int q = 0; q < 4; ++q) r16 = p130_mul(r16, r16);
+  P130 r4 = p130_mul(r, r);
+  r4 = p130_mul(r4, r4);
+  for (int t = 0; t < 256; ++t) {
+    const P130 f = p130_carry(p130_pow(r4, (uint32_t)(255 - t)));
+    for (int u = 0; u < 5; ++u) pw[t * 5 + u] = f.v[u];
+  }
+  P130 r16 = p130_mul(r4, r4);
+  r16 = p130_mul(r16, r16);
   std::vector<P130> rp(64);
   for (int t = 0; t < 64; ++t) rp[t] = p130_carry(p130_pow(r16, (uint32_t)(63 - t)));
   int8_t* tab = reinterpret_cast<int8_t*>(pw.data() + kPowTabOff);
@@ -266,6 +171,92 @@ static void emul_mac_fused(uint32_t (&tag)[4], const MsgKey& key, const uint8_t*
     const P130 q128 = p130_carry(p130_mul(carry64(d), p130_bit(128)));
     for (int u = 0; u < 5; ++u) pw[kPowQOff + T * 5 + u] = q128.v[u];
   }
+  return pw;
+}
+
+// emulate k_poly_powers tables + k_mac_horner (first / last chunk) + the matrix-core
+// k_mac_chunks<0> (middle chunks as 16 interleaved rows; the MFMA is an explicit
+// integer dot product) + k_mac_final
+static void emul_mac_mfma(uint32_t (&tag)[4], const MsgKey& key, const uint8_t* ctbytes, uint32_t N) {
+  const int C = kChunkBytes;
+  const int K = (int)(((int64_t)N + 32 + C - 1) / C);
+  const int last = (int)(((int64_t)N + 31) / C);
+  const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
+  const P130 r = p130_r_from_key(rk);
+  const std::vector<uint32_t> pw = emul_tables(r);
+  const int8_t* tab = reinterpret_cast<const int8_t*>(pw.data() + kPowTabOff);
+  std::vector<P130> parts(K);
+  for (int k = 0; k < K; ++k) {
+    std::vector<uint8_t> buf(C, 0xAA);
+    const int64_t kC = (int64_t)k * C;
+    const int64_t start = kC >= 32 ? kC - 32 : 0;
+    const int64_t end = std::min((int64_t)N, kC + C - 32);
+    if (start >= end) { parts[k] = p130_zero(); continue; }
+    for (int64_t pos = start; pos < end; ++pos) buf[pos - (kC - 32)] = ctbytes[pos];
+    const int64_t fb = start / 16, eb = (end + 15) / 16;
+    uint64_t d[5] = {0, 0, 0, 0, 0};
+    if (k != 0 && k != last) {  // middle: 16 "MFMA" rows
+      for (int i = 0; i < 16; ++i) {
+        int32_t c[kPolyDigits];
+        for (int dd = 0; dd < kPolyDigits; ++dd) {
+          int32_t acc = 0;
+          for (int t = 0; t < 64; ++t)
+            for (int b = 0; b < 16; ++b)
+              acc += (int32_t)(int8_t)(buf[16 * (i + 16 * t) + b] ^ 0x80) * tab[dd * kSegBytes + 16 * t + b];
+          c[dd] = acc;
+        }
+        P130 kseg;
+        for (int u = 0; u < 5; ++u) kseg.v[u] = pw[kPowKsegOff + u] + pw[kPowQOff + 64 * 5 + u];
+        const uint32_t* rf = pw.data() + kPowRowOff + i * 5;
+        const P130 h = p130_mul(poly_seg_value(c, p130_carry(kseg)), P130{{rf[0], rf[1], rf[2], rf[3], rf[4]}});
+        for (int u = 0; u < 5; ++u) d[u] += h.v[u];
+      }
+    } else {  // k_mac_horner: lane t sums the 4 blocks ending 4 (255 - t) blocks before eb
+      for (int tid = 0; tid < 256; ++tid) {
+        P130 hh = p130_zero();
+        for (int q = 0; q < 4; ++q) {
+          const int64_t i = eb - 4 * (int64_t)(256 - tid) + q;
+          P130 cb = p130_zero();
+          if (i >= fb) cb = load_block(buf.data(), i, kC, N);
+          hh = p130_mul(p130_add(hh, cb), r);
+        }
+        const uint32_t* pf = pw.data() + tid * 5;
+        hh = p130_mul(hh, P130{{pf[0], pf[1], pf[2], pf[3], pf[4]}});
+        for (int u = 0; u < 5; ++u) d[u] += hh.v[u];
+      }
+    }
+    parts[k] = carry64(d);
+  }
+  const P130 rC = p130_pow(r, C / 16);
+  P130 H = p130_zero();
+  int64_t prev = 0;
+  for (int k = 0; k < K; ++k) {
+    const int64_t e = (k < K - 1) ? ((int64_t)(k + 1) * C - 32) / 16 : ((int64_t)N + 15) / 16;
+    if (k == 0) H = parts[k];
+    else {
+      const int64_t dd = e - prev;
+      const P130 Rd = (dd == C / 16) ? rC : p130_pow(r, (uint32_t)dd);
+      H = p130_carry(p130_add(p130_mul(H, Rd), parts[k]));
+    }
+    prev = e;
+  }
+  const uint32_t s4[4] = {key.poly_s[0], key.poly_s[1], key.poly_s[2], key.poly_s[3]};
+  p130_finish(tag, H, s4);
+}
+
+// emulate the seal-side MAC that k_encode_encrypt computes per tile (interleaved
+// rows cut by the tile borders), k_mac_horner for the first
+// and last chunk (by the definition of a chunk partial) and k_mac_final. `cuts` are
+// the tile borders (message byte offsets, ascending, first 0, last N).
+static void emul_mac_fused(uint32_t (&tag)[4], const MsgKey& key, const uint8_t* ctbytes, uint32_t N,
+                           const std::vector<uint32_t>& cuts) {
+  const int C = kChunkBytes;
+  const int K = (int)(((int64_t)N + 32 + C - 1) / C);
+  const int last = (int)(((int64_t)N + 31) / C);
+  const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
+  const P130 r = p130_r_from_key(rk);
+  const std::vector<uint32_t> pw = emul_tables(r);
+  const int8_t* tab = reinterpret_cast<const int8_t*>(pw.data() + kPowTabOff);
   // ---- tiles
   std::vector<uint32_t> partials((size_t)K * 8, 0);
   for (size_t ti = 0; ti + 1 < cuts.size(); ++ti) {

@@ -35,26 +35,24 @@ constexpr int kSubBytes = 1024;     // terminator-count granularity (16 lanes x 
 constexpr int kSubPerChunk = kChunkBytes / kSubBytes;
 constexpr int kSumTile = 6144;      // elements per decode-sum tile (~11 KiB of varints at m = 433)
 
-// Per-message Poly1305 tables (k_poly_powers), kPowWords u32 per message:
-//   [0, 1280)         chunk factors r^(4(255-t)), t < 256, 5 x 26-bit limbs
-//   [1280, 1288)      segment constant K_seg (5 limbs; see seal.hip)
-//   [1288, kPowWords) int8 weight digits [kPolyDigits][kSegBytes]: 7-bit digit d of
-//                     W(pos) = 2^(8 (pos % 16)) r^(64 - pos / 16) mod p
-constexpr int kSegBytes = 1024;     // MFMA MAC row: one 64-block segment
+// Per-message Poly1305 tables (k_poly_powers), kPowWords u32 per message. The
+// matrix-core MAC takes a 16 KiB chunk as 16 interleaved rows: row i = blocks
+// i, i + 16, i + 32, ... (so 16 lanes read 256 contiguous bytes), K index
+// 16 t + a = byte a of block i + 16 t; R = r^16.
+//   [0, 1280)           chunk factors r^(4(255-t)), t < 256, 5 x 26-bit limbs (Horner lanes)
+//   [kPowKsegOff, +5)   row constant without the pad bits: 128 sum W - 2^24 sum_d 2^(7d)
+//   [kPowTabOff, ...)   int8 weight digits [kPolyDigits][kSegBytes]: 7-bit digit d of
+//                       W(16 t + a) = 2^(8a) R^(63 - t) mod p
+//   [kPowRowOff, +80)   row factors r^(16 - i), i < 16 (5 limbs each)
+//   [kPowQOff, +325)    pad-bit prefixes 2^128 sum_{t' < T} R^(63 - t'), T = 0..64 (a
+//                       whole row: entry 64; a row cut by a tile border: a difference)
+constexpr int kSegBytes = 1024;     // MFMA MAC row: 64 blocks
 constexpr int kPolyDigits = 19;     // 7-bit digits of a value < 2^133
 constexpr int kPowKsegOff = 256 * 5;
 constexpr int kPowTabOff = kPowKsegOff + 8;
 constexpr int kPowRowOff = kPowTabOff + kPolyDigits * kSegBytes / 4;
 constexpr int kPowQOff = kPowRowOff + 16 * 5;
 constexpr int kPowWords = (kPowQOff + 65 * 5 + 7) / 8 * 8;
-// Seal-side variant of the tables (k_poly_powers with interleaved != 0), for the MAC
-// that k_encode_encrypt computes on its tile while the ciphertext is still in LDS.
-// Row i of a 16 KiB chunk takes the blocks i, i + 16, i + 32, ... (so 16 lanes read
-// 256 contiguous LDS bytes), K index 16 t + a = byte a of block i + 16 t:
-//   digits            of W(16 t + a) = 2^(8a) R^(63 - t) mod p, R = r^16
-//   [kPowKsegOff, +5) the row constant without the pad bits, 128 sum W - 2^24 sum_d 2^(7d)
-//   [kPowRowOff, +80) row factors r^(16 - i), i < 16 (5 limbs each)
-//   [kPowQOff, +325)  pad-bit prefixes 2^128 sum_{t' < T} R^(63 - t'), T = 0..64
 
 // Error bits (device error word)
 enum ErrBits : uint32_t {
@@ -132,7 +130,7 @@ void launch_chacha_mask_sum(int P, int D, uint32_t m, int seed_words, const uint
 // Segmented exclusive scan of rows [M][T] in place; totals[M] = row sums.
 void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, hipStream_t s);
 // Varint-encode + XSalsa20-encrypt tiles into the arena (ct bytes only). With
-// `pows` (interleaved tables), `pt_len` and zeroed `partials` [M][K][8] non-null,
+// `pows`, `pt_len` and zeroed `partials` [M][K][8] non-null,
 // every tile also adds its share of the Poly1305 partials of the message's middle
 // chunks (all but the first and the last) to `partials`; launch_mac_edges then
 // supplies those two and launch_mac_final the tag.
@@ -140,15 +138,14 @@ void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
                            const uint32_t* tile_off, const MsgKey* keys, uint8_t* ct,
                            uint64_t stride, const uint32_t* pows, const uint32_t* pt_len,
                            uint32_t* partials, int K, hipStream_t s);
-// Poly1305 partials of every message's first and last chunk only (per-lane Horner;
-// needs only the chunk factors of `pows`, present in both table variants).
+// Poly1305 partials of every message's first and last chunk only (per-lane Horner).
 void launch_mac_edges(int M, int K, const MsgKey* keys, const uint32_t* pows, const uint8_t* ct,
                       uint64_t stride, const uint32_t* pt_len, uint32_t* partials, hipStream_t s);
 // Poly1305 chunk partials (and, when decrypt!=0, in-place decryption plus
 // varint-terminator counts per chunk).
 // Per-message Poly1305 tables pows [M][kPowWords]: chunk factors, segment
 // constant and weight digits of the matrix-core MAC (layout above).
-void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, int interleaved, hipStream_t s);
+void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s);
 // With decrypt, term_cnt [M][K] (per chunk) and/or sub_cnt [M][K * kSubPerChunk]
 // (per 1 KiB sub-chunk) receive terminator counts (either may be null).
 void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,

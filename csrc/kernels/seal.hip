@@ -7,13 +7,14 @@
 //
 // Parallel Poly1305: a message is cut into 16 KiB chunks aligned to the keystream
 // (chunk k covers keystream bytes [kC, (k+1)C), i.e. message bytes
-// [kC-32, (k+1)C-32)). Inside a chunk the 16 segments of 64 blocks (aligned to
-// the chunk's last block) are the rows of an int8 GEMM against the message's
-// weight digits on the matrix cores (v_mfma_i32_16x16x64_i8; the algebra is in
-// device_crypto.hpp, poly_seg_value); segments holding a partial block or the
-// message start fall back to per-lane Horner over 4 blocks. Segment / lane sums
-// are placed by per-message factors r^(4(255-t)), and a per-message pass chains
-// the chunk partials with r^(C/16).
+// [kC-32, (k+1)C-32)). A middle chunk is 1024 full blocks, taken as 16 interleaved
+// rows (row i = blocks i, i + 16, i + 32, ...: the 16 lanes of an MFMA operand
+// group read 256 contiguous bytes) of an int8 GEMM against the message's weight
+// digits on the matrix cores (v_mfma_i32_16x16x64_i8; the algebra is in
+// device_crypto.hpp, poly_seg_value); a message's first and last chunk (message
+// start, partial final block) are summed by per-lane Horner over 4 blocks. Row
+// values are placed by r^(16 - i), Horner lane sums by r^(4(255-t)), and a
+// per-message pass chains the chunk partials with r^(C/16).
 #include "block_utils.hpp"
 #include "device_crypto.hpp"
 #include "kernels.hpp"
@@ -367,14 +368,13 @@ SDA_DEV P130 block_sum_p130(const P130& h, uint64_t (*red)[kWaves]) {
 
 // Per-message Poly1305 tables (layout: kernels.hpp kPow*):
 //  * r^(4 (255 - t)) for t = 0..255: the factor that places lane t's 4-block
-//    Horner sum (or segment t/16's value, at t = 16 s + 15) at its distance
-//    from the chunk end, so a chunk's combine is one multiply per term;
-//  * the 7-bit digits of the segment weights W(pos) and the segment constant
-//    K_seg of the matrix-core MAC (device_crypto.hpp, poly_seg_value).
+//    Horner sum at its distance from the chunk end (k_mac_horner);
+//  * for the matrix-core rows: the 7-bit digits of the weights W(16 t + a), the
+//    row constant, the row factors r^(16 - i) and the pad-bit prefix sums
+//    (device_crypto.hpp, poly_seg_value / poly_row_const).
 // Depends only on the key: computed once per message on the side stream.
 __global__ void __launch_bounds__(kBlock)
-    k_poly_powers(const MsgKey* __restrict__ keys, uint32_t* __restrict__ pows, int prio,
-                  int interleaved) {
+    k_poly_powers(const MsgKey* __restrict__ keys, uint32_t* __restrict__ pows, int prio) {
   if (prio) __builtin_amdgcn_s_setprio(3);  // side-stream key work (see k_seal_setup)
   __shared__ P130 rp[64];
   __shared__ uint64_t red[5][kWaves];
@@ -390,19 +390,14 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
     for (int u = 0; u < 5; ++u) base[t * 5 + u] = f.v[u];
   }
-  // r^(64 - jb) for the segment's blocks jb = 0..63; interleaved rows (kernels.hpp):
-  // R^(63 - t) with R = r^16 for the row's blocks i + 16 t
+  // R^(63 - t), R = r^16, for the blocks i + 16 t of a row
   P130 mine = p130_zero();
   if (t < 64) {
-    if (interleaved) {
-      P130 r16 = p130_mul(r, r);
-      r16 = p130_mul(r16, r16);
-      r16 = p130_mul(r16, r16);
-      r16 = p130_mul(r16, r16);
-      mine = p130_carry(p130_pow(r16, (uint32_t)(63 - t)));
-    } else {
-      mine = p130_carry(p130_pow(r, (uint32_t)(64 - t)));
-    }
+    P130 r16 = p130_mul(r, r);
+    r16 = p130_mul(r16, r16);
+    r16 = p130_mul(r16, r16);
+    r16 = p130_mul(r16, r16);
+    mine = p130_carry(p130_pow(r16, (uint32_t)(63 - t)));
     rp[t] = mine;
   }
   __syncthreads();
@@ -424,14 +419,12 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
   for (int d = 0; d < kPolyDigits; ++d) tab[d * (kSegBytes / 4) + t] = dig[d];
   const P130 sw = block_sum_p130(wsum, red);
-  const P130 sr = block_sum_p130(mine, red);
   if (t == 0) {
-    // interleaved: the pad bits are added per row from the prefix table below
-    const P130 k = poly_kseg(interleaved ? p130_zero() : sr, sw);
+    // the row constant without pad bits: those come from the prefix table below
+    const P130 k = poly_kseg(p130_zero(), sw);
 #pragma unroll
     for (int u = 0; u < 5; ++u) base[kPowKsegOff + u] = k.v[u];
   }
-  if (!interleaved) return;
   if (t < 16) {
     const P130 f = p130_carry(p130_pow(r, (uint32_t)(16 - t)));
 #pragma unroll
@@ -537,13 +530,13 @@ __global__ void __launch_bounds__(kBlock)
 
 // Middle chunks on the matrix cores (+ in-place decryption and terminator
 // counts for every chunk when DECRYPT). A middle chunk (not the message's
-// first or last) is 16 full segments of 64 blocks, segment s = blocks
-// [fb + 64 s, fb + 64 (s + 1)), fb = kC/16 - 2: the 16 rows of an int8 GEMM
-// (device_crypto.hpp, poly_seg_value) with K = the segment's 1 KiB of bytes
-// (wave w takes bytes [256 w, 256 w + 256) of every row) and N = the 19 weight
-// digits (two 16-column tiles). Row s is then placed by r^(64 (15 - s)) =
-// factor t = 16 s + 15. First / last chunks are k_mac_horner's (launched
-// first: it reads the ciphertext this kernel decrypts in place).
+// first or last) is 1024 full blocks starting at block fb = kC/16 - 2, taken as
+// 16 interleaved rows (row i = blocks fb + i + 16 t, t < 64): the 16 rows of an
+// int8 GEMM (device_crypto.hpp, poly_seg_value) with K = the row's 1 KiB of bytes
+// (wave w takes t in [16 w, 16 w + 16) of every row) and N = the 19 weight
+// digits (two 16-column tiles). Row i is then placed by r^(16 - i). First / last
+// chunks are k_mac_horner's (launched first: it reads the ciphertext this kernel
+// decrypts in place).
 template <int DECRYPT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
     k_mac_chunks(int K, const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
@@ -609,10 +602,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     const bool middle = use_mfma && k != 0 && k != last;
     v4i a[4];
     if (middle) {
-      const int64_t lo = kC / 16 - 2 + 64 * row;  // first block of segment `row`
+      // row `row` = blocks row + 16 t of the chunk: 16 lanes read 256 contiguous bytes
+      const int64_t fb = kC / 16 - 2;
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq)
-        a[qq] = *reinterpret_cast<const v4i*>(gmsg + 16 * (lo + 4 * (4 * wave + qq) + g));
+        a[qq] = *reinterpret_cast<const v4i*>(gmsg + 16 * (fb + row + 16 * (4 * (4 * wave + qq) + g)));
     }
     // The keystream needs no loaded byte: computed here, its ~1000 instructions
     // run while the chunk's loads (issued above) are in flight.
@@ -710,14 +704,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
       int32_t c[kPolyDigits];
 #pragma unroll
       for (int d = 0; d < kPolyDigits; ++d) c[d] = cacc[kk][s][d];
+      // every pad bit of the chunk is this block's: prefix table entry 64; placed by r^(16 - s)
       P130 kseg, sfac;
-      const uint32_t* pf = pw + (16 * s + 15) * 5;
+      const uint32_t* pf = pw + kPowRowOff + s * 5;
 #pragma unroll
       for (int u = 0; u < 5; ++u) {
-        kseg.v[u] = pw[kPowKsegOff + u];
+        kseg.v[u] = pw[kPowKsegOff + u] + pw[kPowQOff + 64 * 5 + u];
         sfac.v[u] = pf[u];
       }
-      h = p130_mul(poly_seg_value(c, kseg), sfac);
+      h = p130_mul(poly_seg_value(c, p130_carry(kseg)), sfac);
     }
     uint64_t d[5];
 #pragma unroll
@@ -820,10 +815,9 @@ void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
 
 extern int g_powers_prio;  // keys.hip (set_key_prio)
 
-void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, int interleaved, hipStream_t s) {
+void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s) {
   if (M <= 0) return;
-  hipLaunchKernelGGL(k_poly_powers, dim3(M), dim3(kBlock), 0, s, keys, pows, g_powers_prio,
-                     interleaved);
+  hipLaunchKernelGGL(k_poly_powers, dim3(M), dim3(kBlock), 0, s, keys, pows, g_powers_prio);
 }
 
 void launch_mac_edges(int M, int K, const MsgKey* keys, const uint32_t* pows, const uint8_t* ct,

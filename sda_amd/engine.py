@@ -29,7 +29,7 @@ from ._native import native
 from .models.schemes import Additive, AggregationSpec, ChaChaMask, FullMask, PackedShamir
 from .ops import gpu as G
 from .ops.sealed import (Arena, KeySet, open_, open_data, open_setup, open_sum, seal, seal_data,
-                         seal_encode, seal_mac, seal_setup)
+                         seal_setup)
 from .utils.trace import tracing_enabled
 
 _TRACE = tracing_enabled()
@@ -38,8 +38,6 @@ _TRACE = tracing_enabled()
 _OPEN_AFTER_SHARE = os.environ.get("SDA_OPEN_AFTER_SHARE", "1") == "1"
 # "open,powers" wave priorities of the side-stream key kernels (experiments)
 _KEY_PRIO = os.environ.get("SDA_KEY_PRIO")
-# Experimental: the seal-side tag pass per clerk on its own stream (see _participate)
-_MAC_OVERLAP = os.environ.get("SDA_MAC_OVERLAP", "0") == "1"
 
 
 class AggregationError(RuntimeError):
@@ -49,7 +47,7 @@ class AggregationError(RuntimeError):
 _SIDE_STREAMS: dict = {}
 
 
-def concurrent_stream(device, tries: int = 12, spin_us: int = 250, slot: int = 0) -> "torch.cuda.Stream":
+def concurrent_stream(device, tries: int = 12, spin_us: int = 250) -> "torch.cuda.Stream":
     """A stream whose kernels really run beside the current stream's.
 
     HIP multiplexes a process's streams onto few hardware queues (4 by default),
@@ -62,7 +60,7 @@ def concurrent_stream(device, tries: int = 12, spin_us: int = 250, slot: int = 0
     queue. Falls back to the last candidate (correct, only slower)."""
     dev = torch.device(device)
     main = torch.cuda.current_stream(dev)
-    key = (dev.index, main.cuda_stream, slot)
+    key = (dev.index, main.cuda_stream)
     if key in _SIDE_STREAMS:
         return _SIDE_STREAMS[key]
     gate = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -254,12 +252,6 @@ class DeviceAggregator:
             self._side = concurrent_stream(self.device)
         return self._side
 
-    def _mac_stream(self):
-        if getattr(self, "_macs", None) is None:
-            self._side_stream()
-            self._macs = concurrent_stream(self.device, slot=1)
-        return self._macs
-
     def _live(self, clerks):
         spec, n = self.spec, self.n
         live = list(range(n)) if clerks is None else sorted(set(int(c) for c in clerks))
@@ -397,37 +389,13 @@ class DeviceAggregator:
             if t is not None:
                 t.record_stream(main)
         main.wait_event(ev_sealkeys)
-        ev_mac = None
-        if _MAC_OVERLAP and cnt is not None and len(live) == n:
-            # per clerk: encode on the main stream, the HBM-bound tag pass over the
-            # stored ciphertext on a stream of its own beside the next clerk's encode
-            macs = self._mac_stream()
-            ev_mac = []
-            sh2, cnt2 = shares.view(n * P, B), cnt.view(n * P, -1)
-            for c in range(n):
-                box, kc = clerk_arena.slice(c * P, P), ks_clerk.slice(c * P, P)
-                kc, part = seal_encode(box, kc, sh2[c * P:(c + 1) * P], cnt2[c * P:(c + 1) * P])
-                if c == 0:
-                    self._inject_corruption(clerk_arena)
-                ev = torch.cuda.Event()
-                ev.record(main)
-                with torch.cuda.stream(macs):
-                    macs.wait_event(ev)
-                    seal_mac(box, kc, part, err)
-                    e2 = torch.cuda.Event()
-                    e2.record(macs)
-                    ev_mac.append(e2)
-            clerk_arena.ct.record_stream(macs)
-            clerk_arena.pt_len.record_stream(macs)
-            ks_clerk.record_stream(macs)
-        else:
-            seal_data(clerk_arena, ks_clerk, shares.view(n * P, B), err, cnt)
-            self._inject_corruption(clerk_arena)
+        seal_data(clerk_arena, ks_clerk, shares.view(n * P, B), err, cnt)
+        self._inject_corruption(clerk_arena)
         del shares
         if mask_arena is not None:
             seal_data(mask_arena, ks_mask, mask_vals, err, mask_cnt)
         return {"P": P, "kidx": kidx_clerk, "ev_openkeys": ev_openkeys, "mask_arena": mask_arena,
-                "ko_mask": ko_mask, "inbox": clerk_arena, "ko_clerk": ko_clerk, "ev_mac": ev_mac}
+                "ko_mask": ko_mask, "inbox": clerk_arena, "ko_clerk": ko_clerk}
 
     def _clerk(self, st, live, err):
         """Open + combine an inbox (the local arena or the routed one)."""
@@ -436,17 +404,7 @@ class DeviceAggregator:
         main.wait_event(st["ev_openkeys"])
         inbox = st.pop("inbox")
         ko_clerk = st["ko_clerk"]
-        ev_mac = st.get("ev_mac")
-        if ev_mac is not None:
-            # clerk c's boxes are complete once their tags are written; the last
-            # clerk's tag pass runs beside the first clerk's open
-            combined = torch.empty(len(live), self.spec.batches, dtype=torch.int32, device=self.device)
-            keys = ko_clerk[0] if isinstance(ko_clerk, list) else ko_clerk
-            for c in range(self.n):
-                main.wait_event(ev_mac[c])
-                open_sum(inbox.slice(c * P, P), keys.slice(c * P, P), err, rows=1, out=combined[c])
-        else:
-            combined = self._open_combine(inbox, ko_clerk, live, P, err)
+        combined = self._open_combine(inbox, ko_clerk, live, P, err)
         del inbox
         # recipient's share of the mask work is data-parallel too: open these
         # participants' mask boxes and sum them

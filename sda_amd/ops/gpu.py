@@ -232,9 +232,8 @@ def segscan(data: torch.Tensor, totals: torch.Tensor | None):
 def encode_encrypt(vals, tile_off, keys, ct, stride, mac=None):
     """Varint-encode + encrypt the rows of `vals` into the arena. `mac` =
     (pows, pt_len, partials, K) fuses the Poly1305 of the middle chunks into the
-    pass: `pows` must be the interleaved tables (``poly_powers(...,
-    interleaved=True)``) and `partials` zeroed; :func:`mac_edges` and
-    :func:`mac_final` complete the tag."""
+    pass (`partials` zeroed); :func:`mac_edges` and :func:`mac_final` complete
+    the tag."""
     M, L = vals.shape
     _check(vals, "vals", VALUE_DTYPES)
     _check(tile_off, "tile_off", torch.int32, numel=M * tiles(L))
@@ -252,13 +251,12 @@ def encode_encrypt(vals, tile_off, keys, ct, stride, mac=None):
                           _ptr(ct), stride, pows, pt_len, partials, K, _stream())
 
 
-def poly_powers(M, keys, pows, interleaved: bool = False):
-    """Per-message Poly1305 tables; `interleaved` selects the seal-side layout read
-    by the fused MAC of :func:`encode_encrypt` (the chunk factors that
-    `mac_edges` / the Horner kernel read are the same in both)."""
+def poly_powers(M, keys, pows):
+    """Per-message Poly1305 tables (chunk factors for the Horner lanes; weight
+    digits, row factors and pad-bit prefixes for the matrix-core rows)."""
     _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
     _check(pows, "pows", torch.int32, min_numel=M * POW_WORDS)
-    _gpu().poly_powers(M, _ptr(keys), _ptr(pows), 1 if interleaved else 0, _stream())
+    _gpu().poly_powers(M, _ptr(keys), _ptr(pows), _stream())
 
 
 def mac_edges(M, K, keys, pows, ct, stride, pt_len, partials):

@@ -88,17 +88,12 @@ class Arena:
 class KeySet:
     """Per-message derived keys: the 80-byte `MsgKey` records (XSalsa20 subkey,
     nonce tail, Poly1305 r/s) and each message's Poly1305 tables (chunk factors
-    r^(4(255-t)) plus the weight digits of the matrix-core MAC). Both depend only
-    on the key agreement, so they are produced together on the side stream.
-
-    `sealing` key sets get the interleaved-row tables that the fused MAC of the
-    encode kernel reads (unless that fusion is switched off); opening ones the
-    contiguous-segment tables of `k_mac_chunks`."""
+    r^(4(255-t)) plus the weight digits, row factors and pad-bit prefixes of the
+    matrix-core MAC). Both depend only on the key agreement, so they are
+    produced together on the side stream."""
     M: int
     keys: torch.Tensor  # uint8 [M * MSGKEY_BYTES]
     pows: torch.Tensor | None  # int32 [M * POW_WORDS]; None = not derived yet
-    sealing: bool = False
-    interleaved: bool = False  # layout of `pows`
 
     @classmethod
     def derive(cls, M: int, keys: torch.Tensor) -> "KeySet":
@@ -109,9 +104,8 @@ class KeySet:
         if self.pows is not None:
             return self
         pows = torch.empty(self.M * G.POW_WORDS, dtype=torch.int32, device=self.keys.device)
-        il = self.sealing and FUSED_SEAL_MAC
-        G.poly_powers(self.M, self.keys, pows, interleaved=il)
-        return KeySet(self.M, self.keys, pows, self.sealing, il)
+        G.poly_powers(self.M, self.keys, pows)
+        return KeySet(self.M, self.keys, pows)
 
     def slice(self, first: int, count: int) -> "KeySet":
         """Keys of messages [first, first+count) (no copy)."""
@@ -119,8 +113,7 @@ class KeySet:
             raise ValueError("key slice out of range")
         kb, pw = G.MSGKEY_BYTES, G.POW_WORDS
         return KeySet(count, self.keys[first * kb:(first + count) * kb],
-                      None if self.pows is None else self.pows[first * pw:(first + count) * pw],
-                      self.sealing, self.interleaved)
+                      None if self.pows is None else self.pows[first * pw:(first + count) * pw])
 
     def record_stream(self, stream) -> None:
         self.keys.record_stream(stream)
@@ -128,8 +121,11 @@ class KeySet:
             self.pows.record_stream(stream)
 
 
-# The seal-side Poly1305 inside the encode kernel (default). False = a separate
-# MAC pass over the stored ciphertext (k_mac_chunks<0>) -- A/B measurements.
+# The seal-side Poly1305 inside the encode kernel, on the tile while it is still in
+# LDS (k_encode_encrypt<.., true>) instead of a separate pass over the stored
+# ciphertext (k_mac_chunks<0>). Saves 5.5 GB of HBM reads per headline round but
+# measured slower (the encode kernel is issue-bound; +1.4 ms against 1.0 ms saved),
+# so it is off unless SDA_FUSED_SEAL_MAC=1.
 FUSED_SEAL_MAC = os.environ.get("SDA_FUSED_SEAL_MAC", "0") == "1"
 
 
@@ -147,7 +143,7 @@ def seal_setup(arena: Arena, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: 
     keys = torch.empty(arena.M * G.MSGKEY_BYTES, dtype=torch.uint8, device=arena.ct.device)
     G.seal_setup(arena.M, rng_key, owner_base, key_idx, pks, arena.ct, arena.stride, keys, err,
                  gate=gate)
-    return KeySet(arena.M, keys, None, sealing=True)
+    return KeySet(arena.M, keys, None)
 
 
 def seal_encode(arena: Arena, keys: KeySet, values: torch.Tensor,
@@ -170,7 +166,7 @@ def seal_encode(arena: Arena, keys: KeySet, values: torch.Tensor,
     G.segscan(cnt, arena.pt_len)  # cnt becomes the tile byte offsets
     keys = keys.with_powers()
     partials = None
-    if keys.interleaved:
+    if FUSED_SEAL_MAC:
         # one pass: every tile adds its share of the middle chunks' Poly1305 partials
         # while its ciphertext is in LDS; the first / last chunks follow by Horner
         partials = torch.zeros(M * arena.K * 8, dtype=torch.int32, device=dev)
@@ -186,7 +182,7 @@ def seal_mac(arena: Arena, keys: KeySet, partials, err: torch.Tensor) -> Arena:
     header. Reads the stored ciphertext (all of it, or only the first and last
     chunk of every message when the encode pass already did the middle ones)."""
     M, dev = arena.M, arena.ct.device
-    if keys.interleaved:
+    if partials is not None:
         G.mac_edges(M, arena.K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials)
     else:
         partials = torch.empty(M * arena.K * 8, dtype=torch.int32, device=dev)

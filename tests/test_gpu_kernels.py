@@ -36,11 +36,18 @@ def _keytable(native, cuda, count):
     return KeyTable.generate(count, cuda)
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("L,modulus", [(1, 433), (10, 433), (5000, 433), (20000, 433),
-                                       (3000, 2 ** 31 - 1), (70000, 65521)])
-def test_gpu_seal_opens_on_host(cuda, native, L, modulus):
+                                       (3000, 2 ** 31 - 1), (70000, 65521), (150001, 433),
+                                       (40000, 2 ** 31 - 1)])
+def test_gpu_seal_opens_on_host(cuda, native, monkeypatch, L, modulus, fused):
+    """GPU-sealed boxes open on the host. `fused`: the tag's middle chunks computed
+    inside the encode kernel (per tile, in LDS) instead of by a pass over the
+    stored ciphertext -- both must give libsodium's tag."""
     from sda_amd.ops import gpu as G
+    from sda_amd.ops import sealed
     from sda_amd.ops.sealed import seal
+    monkeypatch.setattr(sealed, "FUSED_SEAL_MAC", fused)
     keys = _keytable(native, cuda, 2)
     M = 5
     vdt = G.value_dtype(modulus)
