@@ -87,8 +87,13 @@ def parse():
                     help="N > 1. committee (default): sealed boxes routed to the clerks' GPUs, "
                          "per-rank key custody, sealed results to rank 0. owner: non-private "
                          "upper bound, each GPU opens its own participants' boxes")
-    ap.add_argument("--waves", type=int, default=4,
-                    help="committee layout: participant waves the exchange is pipelined over")
+    ap.add_argument("--waves", type=int, default=0,
+                    help="committee layout: participant waves the exchange is pipelined over. "
+                         "0 (default): with N > 1, 2 / 4 / 8 waves are timed for two untimed rounds "
+                         "each before the warm-up and the fastest is used (more waves start the "
+                         "all-to-all earlier and shorten the exposed last wave, fewer waves keep "
+                         "the grids large: which wins depends on the xGMI rate RCCL reaches); "
+                         "4 on a single rank")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the distributed engine even on one rank (measures its overhead)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -134,6 +139,7 @@ def main():
     spec = AggregationSpec(args.dim, args.modulus, Additive(args.clerks, args.modulus), NoMask(),
                            title="bench")
     P = args.participants
+    waves, wave_tuning = 1, {}
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     secrets = torch.randint(0, args.modulus, (P, args.dim), dtype=torch.int32, device="cuda",
                             generator=gen)
@@ -147,11 +153,28 @@ def main():
     else:
         from sda_amd.parallel.engine import DistributedAggregator
 
+        waves = args.waves if args.waves > 0 else 4
         agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", dev_index),
                                     time_stages=args.stages, layout=args.layout,
-                                    waves=args.waves, force_pipeline=args.force_dist,
+                                    waves=waves, force_pipeline=args.force_dist,
                                     deadline_s=min(60.0, args.dist_timeout / 4))
         engine, comm = agg.engine, agg.comm
+        if args.waves <= 0 and world > 1 and args.layout == "committee":
+            # untimed: pick the pipeline depth on this node's measured exchange rate
+            # (every rank takes the same decision: the times are max-reduced)
+            for w in (2, 4, 8):
+                agg.set_waves(w)
+                agg.run_round(secrets, check=True)
+                comm.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(2):
+                    agg.run_round(secrets, check=False)
+                torch.cuda.synchronize()
+                comm.barrier()
+                wave_tuning[w] = comm.all_reduce_max(time.perf_counter() - t0) / 2 * 1e3
+            waves = min(wave_tuning, key=wave_tuning.get)
+            agg.set_waves(waves)
         # the global reference sum, reduced to rank 0
         total = comm.reduce_sum(secrets.to(torch.int64).sum(0), dst=0)
         expected = torch.remainder(total, args.modulus).to(torch.int32) if rank == 0 else None
@@ -215,7 +238,7 @@ def main():
             parallelism = "single GPU"
         elif args.layout == "committee":
             parallelism = (f"dp{world} participants x committee-sharded clerks: all-to-all of "
-                           f"sealed boxes over xGMI (grouped RCCL send/recv, {args.waves} waves), "
+                           f"sealed boxes over xGMI (grouped RCCL send/recv, {waves} waves), "
                            "per-rank key custody, sealed clerk results gathered on rank 0")
             if world == 1:
                 parallelism += " [distributed engine on one rank: nothing crosses xGMI]"
@@ -246,6 +269,8 @@ def main():
             "data": "synthetic uniform random participant vectors in [0, 433)",
             "hbm_high_water_bytes": hbm_peak,
             "xgmi": xgmi,
+            "pipeline_waves": waves if dist_mode else None,
+            "pipeline_wave_tuning_ms": {str(k): v for k, v in wave_tuning.items()} or None,
             "timed_steps_verified": "device error word of every timed step (OR over steps and "
                                     "ranks) + last round's output vs the plain sum",
             "config": {
