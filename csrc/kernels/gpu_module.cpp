@@ -128,8 +128,9 @@ PYBIND11_MODULE(_sda_gpu, m) {
                            P<uint32_t>(err), S(stream));
     check_launch("chacha_mask_sum");
   });
-  m.def("segscan", [](int M, int T, uintptr_t data, uintptr_t totals, uintptr_t stream) {
-    launch_segscan(M, T, P<uint32_t>(data), P<uint32_t>(totals), S(stream));
+  m.def("segscan", [](int M, int T, uintptr_t data, uintptr_t totals, uint32_t expect,
+                      uintptr_t err, uintptr_t stream) {
+    launch_segscan(M, T, P<uint32_t>(data), P<uint32_t>(totals), expect, P<uint32_t>(err), S(stream));
     check_launch("segscan");
   });
   m.def("encode_encrypt", [](int M, int L, int value_bytes, uintptr_t vals, uintptr_t tile_off,
@@ -158,10 +159,10 @@ PYBIND11_MODULE(_sda_gpu, m) {
                       P<uint32_t>(term_cnt), P<uint32_t>(sub_cnt), S(stream));
     check_launch("mac_chunks");
   });
-  m.def("mac_final", [](int M, int K, uintptr_t keys, uintptr_t ct, uint64_t stride,
+  m.def("mac_final", [](int M, int K, uintptr_t keys, uintptr_t pows, uintptr_t ct, uint64_t stride,
                         uintptr_t pt_len, uintptr_t partials, int verify, uintptr_t ok,
                         uintptr_t err, uintptr_t stream) {
-    launch_mac_final(M, K, P<const MsgKey>(keys), P<uint8_t>(ct), stride,
+    launch_mac_final(M, K, P<const MsgKey>(keys), P<const uint32_t>(pows), P<uint8_t>(ct), stride,
                      P<const uint32_t>(pt_len), P<const uint32_t>(partials), verify,
                      P<uint32_t>(ok), P<uint32_t>(err), S(stream));
     check_launch("mac_final");

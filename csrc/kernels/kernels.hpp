@@ -127,8 +127,10 @@ void launch_chacha_mask_sum(int P, int D, uint32_t m, int seed_words, const uint
                             uint32_t* out, uint32_t* err, hipStream_t s);
 
 // ---- seal.hip --------------------------------------------------------------
-// Segmented exclusive scan of rows [M][T] in place; totals[M] = row sums.
-void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, hipStream_t s);
+// Segmented exclusive scan of rows [M][T] in place; totals[M] = row sums. With
+// `err` non-null, a row whose sum differs from `expect` sets kErrMalformed.
+void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, uint32_t expect, uint32_t* err,
+                    hipStream_t s);
 // Varint-encode + XSalsa20-encrypt tiles into the arena (ct bytes only). With
 // `pows`, `pt_len` and zeroed `partials` [M][K][8] non-null,
 // every tile also adds its share of the Poly1305 partials of the message's middle
@@ -155,8 +157,8 @@ void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, u
 // benchmarking switch.
 void set_mac_mfma(int mode);
 // Combine partials -> tag; mode 0 = write the header mac, 1 = verify (ok[j]).
-void launch_mac_final(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,
-                      const uint32_t* pt_len, const uint32_t* partials, int verify,
+void launch_mac_final(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,
+                      uint64_t stride, const uint32_t* pt_len, const uint32_t* partials, int verify,
                       uint32_t* ok, uint32_t* err, hipStream_t s);
 
 // ---- open.hip --------------------------------------------------------------

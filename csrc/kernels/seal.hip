@@ -292,8 +292,10 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+// `err` (may be null): a row whose sum is not `expect` raises kErrMalformed there.
 __global__ void __launch_bounds__(kBlock) k_segscan(int T, uint32_t* __restrict__ data,
-                                                    uint32_t* __restrict__ totals) {
+                                                    uint32_t* __restrict__ totals, uint32_t expect,
+                                                    uint32_t* err) {
   __shared__ uint32_t scratch[kWaves];
   uint32_t* row = data + (size_t)blockIdx.x * T;
   uint32_t carry = 0;
@@ -306,6 +308,7 @@ __global__ void __launch_bounds__(kBlock) k_segscan(int T, uint32_t* __restrict_
     carry += tot;
   }
   if (threadIdx.x == 0 && totals) totals[blockIdx.x] = carry;
+  if (threadIdx.x == 0 && err && carry != expect) atomicOr(err, kErrMalformed);
 }
 
 // Read 16 ciphertext bytes as a Poly1305 block (block index i of a message of N
@@ -736,34 +739,70 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   }
 }
 
-__global__ void __launch_bounds__(64)
-    k_mac_final(int M, int K, const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct,
-                uint64_t stride, const uint32_t* __restrict__ pt_len,
+// Chunk partials -> tag, a wave per message. With n chunks before the last one,
+//   H = (sum_{k<n} part_k rC^(n-1-k)) r^(d_last) + part_n,   rC = r^(C/16),
+// d_last = the last chunk's length in blocks. Lane l folds the q = ceil(n/64)
+// chunks [n - (64-l) q, n - (63-l) q) by Horner (chunks are aligned to the end, so
+// every lane's sum sits q chunks before the next lane's), six pairwise steps with
+// F = rC^q, F^2, ... bring the sum to lane 63, which finishes the tag. A serial
+// chain over all chunks took 70 us however few the messages (113 dependent
+// 130-bit multiplies at the headline size).
+SDA_DEV P130 p130_shfl_up(const P130& a, int delta) {
+  P130 o;
+#pragma unroll
+  for (int u = 0; u < 5; ++u) o.v[u] = __shfl_up(a.v[u], delta, 64);
+  return o;
+}
+
+__global__ void __launch_bounds__(kBlock)
+    k_mac_final(int M, int K, const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
+                uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
                 const uint32_t* __restrict__ partials, int verify, uint32_t* __restrict__ ok,
                 uint32_t* err) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= M) return;
+  const int j = blockIdx.x * kWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (j >= M) return;  // wave-uniform
   const uint32_t N = pt_len[j];
   const MsgKey key = keys[j];
   const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
   const P130 r = p130_r_from_key(rk);
-  const int Kc = (int)(((int64_t)N + 32 + kChunkBytes - 1) / kChunkBytes);
-  const P130 rC = p130_pow(r, kChunkBytes / 16);
-  P130 H = p130_zero();
-  int64_t prev = 0;
-  for (int k = 0; k < Kc && k < K; ++k) {
-    const int64_t e = (k < Kc - 1) ? ((int64_t)(k + 1) * kChunkBytes - 32) / 16 : ((int64_t)N + 15) / 16;
+  const uint32_t* pw = pows + (size_t)j * kPowWords;  // chunk factors r^(4 (255 - t))
+  auto factor = [&](int t) { return P130{{pw[t * 5], pw[t * 5 + 1], pw[t * 5 + 2], pw[t * 5 + 3], pw[t * 5 + 4]}}; };
+  auto part = [&](int k) {
     const uint32_t* pp = partials + ((size_t)j * K + k) * 8;
-    P130 hk = P130{{pp[0], pp[1], pp[2], pp[3], pp[4]}};
-    if (k == 0) {
-      H = hk;
-    } else {
-      const int64_t d = e - prev;
-      const P130 Rd = (d == kChunkBytes / 16) ? rC : p130_pow(r, (uint32_t)d);
-      H = p130_carry(p130_add(p130_mul(H, Rd), hk));
+    return P130{{pp[0], pp[1], pp[2], pp[3], pp[4]}};
+  };
+  const int Kc = (int)(((int64_t)N + 32 + kChunkBytes - 1) / kChunkBytes);
+  // chunks past the partials' capacity cannot be summed: such a box fails its check
+  const int n = min(Kc, K) - 1;
+  P130 H = part(n);  // the last chunk's (the only one's when n == 0)
+  if (n > 0) {
+    const P130 rC = p130_mul(factor(0), factor(254));  // r^1020 r^4
+    const int q = (n + 63) / 64;
+    P130 h = p130_zero();
+    for (int i = 0; i < q; ++i) {
+      const int k = n - (64 - lane) * q + i;
+      if (k >= 0) h = p130_carry(p130_add(p130_mul(h, rC), part(k)));
     }
-    prev = e;
+    P130 F = p130_pow(rC, (uint32_t)q);
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const int step = 1 << s;
+      const P130 lower = p130_shfl_up(h, step);
+      if ((lane & (2 * step - 1)) == 2 * step - 1) h = p130_carry(p130_add(p130_mul(lower, F), h));
+      F = p130_mul(F, F);
+    }
+    // the last chunk's length in blocks (C/16 for a full one)
+    const int64_t e_prev = ((int64_t)n * kChunkBytes - 32) / 16;
+    const int64_t e_last = Kc <= K ? ((int64_t)N + 15) / 16 : e_prev + kChunkBytes / 16;
+    const int d = (int)(e_last - e_prev);
+    P130 Rd = rC;
+    if (d < kChunkBytes / 16) {
+      Rd = (d >> 2) ? factor(255 - (d >> 2)) : P130{{1, 0, 0, 0, 0}};
+      for (int b = 0; b < (d & 3); ++b) Rd = p130_mul(Rd, r);
+    }
+    H = p130_carry(p130_add(p130_mul(h, Rd), H));
   }
+  if (lane != 63) return;
   const uint32_t s4[4] = {key.poly_s[0], key.poly_s[1], key.poly_s[2], key.poly_s[3]};
   uint32_t tag[4];
   p130_finish(tag, H, s4);
@@ -782,9 +821,10 @@ __global__ void __launch_bounds__(64)
 
 }  // namespace
 
-void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, hipStream_t s) {
+void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, uint32_t expect, uint32_t* err,
+                    hipStream_t s) {
   if (M <= 0) return;
-  hipLaunchKernelGGL(k_segscan, dim3(M), dim3(kBlock), 0, s, T, data, totals);
+  hipLaunchKernelGGL(k_segscan, dim3(M), dim3(kBlock), 0, s, T, data, totals, expect, err);
 }
 
 template <typename VT>
@@ -847,12 +887,12 @@ void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, u
                        pt_len, partials, term_cnt, sub_cnt, g_mac_mfma);
 }
 
-void launch_mac_final(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,
-                      const uint32_t* pt_len, const uint32_t* partials, int verify,
+void launch_mac_final(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,
+                      uint64_t stride, const uint32_t* pt_len, const uint32_t* partials, int verify,
                       uint32_t* ok, uint32_t* err, hipStream_t s) {
-  if (M <= 0) return;
-  hipLaunchKernelGGL(k_mac_final, dim3((M + 63) / 64), dim3(64), 0, s, M, K, keys, ct, stride,
-                     pt_len, partials, verify, ok, err);
+  if (M <= 0 || K <= 0) return;
+  hipLaunchKernelGGL(k_mac_final, dim3((M + kWaves - 1) / kWaves), dim3(kBlock), 0, s, M, K, keys,
+                     pows, ct, stride, pt_len, partials, verify, ok, err);
 }
 
 }  // namespace sdagpu

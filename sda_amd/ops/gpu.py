@@ -221,12 +221,21 @@ def chacha_mask_sum(seeds: torch.Tensor, D: int, modulus: int, out: torch.Tensor
     _gpu().chacha_mask_sum(P, D, modulus, w, _ptr(seeds), _ptr(out), _ptr(err), _stream())
 
 
-def segscan(data: torch.Tensor, totals: torch.Tensor | None):
+def segscan(data: torch.Tensor, totals: torch.Tensor | None, expect: int | None = None,
+            err: torch.Tensor | None = None):
+    """Exclusive scan of every row of `data` [M][T] in place; `totals` [M] gets the
+    row sums. With `expect` and `err`, a row that does not sum to `expect` sets
+    the malformed bit of the error word."""
     M, T = data.shape
     _check(data, "data", torch.int32)
     if totals is not None:
         _check(totals, "totals", torch.int32, numel=M)
-    _gpu().segscan(M, T, _ptr(data), _ptr(totals) if totals is not None else 0, _stream())
+    e = 0
+    if expect is not None:
+        _check(err, "err", torch.int32, numel=1)
+        e = _ptr(err)
+    _gpu().segscan(M, T, _ptr(data), _ptr(totals) if totals is not None else 0,
+                   int(expect or 0) & 0xFFFFFFFF, e, _stream())
 
 
 def encode_encrypt(vals, tile_off, keys, ct, stride, mac=None):
@@ -292,12 +301,16 @@ def mac_chunks(M, K, keys, pows, ct, stride, pt_len, partials, decrypt, term_cnt
                       _ptr(sub_cnt) if sub_cnt is not None else 0, _stream())
 
 
-def mac_final(M, K, keys, ct, stride, pt_len, partials, verify, ok=None, err=None):
+def mac_final(M, K, keys, pows, ct, stride, pt_len, partials, verify, ok=None, err=None):
+    _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
+    _check(pows, "pows", torch.int32, min_numel=M * POW_WORDS)
+    _check(ct, "ct", torch.uint8, min_numel=M * stride)
+    _check(pt_len, "pt_len", torch.int32, numel=M)
     _check(partials, "partials", torch.int32, numel=M * K * 8)
     _check(err, "err", torch.int32, numel=1)
     if ok is not None:
         _check(ok, "ok", torch.int32, numel=M)
-    _gpu().mac_final(M, K, _ptr(keys), _ptr(ct), stride, _ptr(pt_len), _ptr(partials),
+    _gpu().mac_final(M, K, _ptr(keys), _ptr(pows), _ptr(ct), stride, _ptr(pt_len), _ptr(partials),
                      1 if verify else 0, _ptr(ok) if ok is not None else 0, _ptr(err), _stream())
 
 

@@ -188,7 +188,7 @@ def seal_mac(arena: Arena, keys: KeySet, partials, err: torch.Tensor) -> Arena:
         partials = torch.empty(M * arena.K * 8, dtype=torch.int32, device=dev)
         G.mac_chunks(M, arena.K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
                      decrypt=False)
-    G.mac_final(M, arena.K, keys.keys, arena.ct, arena.stride, arena.pt_len, partials, verify=False,
+    G.mac_final(M, arena.K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials, verify=False,
                 err=err)
     return arena
 
@@ -233,11 +233,9 @@ def open_data(arena: Arena, keys: KeySet, err: torch.Tensor,
     term = torch.empty(M, K, dtype=torch.int32, device=dev)
     G.mac_chunks(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
                  decrypt=True, term_cnt=term)
-    G.mac_final(M, K, keys.keys, arena.ct, arena.stride, arena.pt_len, partials, verify=True, err=err)
+    G.mac_final(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials, verify=True, err=err)
     totals = torch.empty(M, dtype=torch.int32, device=dev)
-    G.segscan(term, totals)
-    # exactly L values per message, otherwise malformed
-    err.bitwise_or_((totals != L).any().to(torch.int32) * 4)
+    G.segscan(term, totals, expect=L, err=err)  # exactly L values per message, else malformed
     if out is None:
         out = torch.empty(M, L, dtype=out_dtype or G.value_dtype(arena.modulus), device=dev)
     G.decode(M, K, L, arena.modulus, arena.ct, arena.stride, arena.pt_len, term, out, err)
@@ -269,10 +267,10 @@ def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
     pre = torch.empty(M, S, dtype=torch.int32, device=dev)
     G.mac_chunks(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
                  decrypt=True, sub_cnt=pre)
-    G.mac_final(M, K, keys.keys, arena.ct, arena.stride, arena.pt_len, partials, verify=True, err=err)
+    G.mac_final(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials, verify=True, err=err)
     totals = torch.empty(M, dtype=torch.int32, device=dev)
-    G.segscan(pre, totals)  # sub-chunk counts -> exclusive ranks
-    err.bitwise_or_((totals != L).any().to(torch.int32) * 4)
+    # sub-chunk counts -> exclusive ranks; exactly L values per message, else malformed
+    G.segscan(pre, totals, expect=L, err=err)
     T = G.sum_tiles(L)
     tile_sub = torch.empty(M, T + 1, dtype=torch.int32, device=dev)
     G.locate_tiles(pre, totals, L, tile_sub)

@@ -24,7 +24,7 @@ boxes) derive their open keys while the waves are still being sealed.
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import List, Optional
 
 import torch
 
@@ -130,6 +130,8 @@ class DeviceCommittee:
                 ctx.res_in = Arena.empty(len(live), B, m, dev)
                 kidx_r = torch.full((len(live),), n, dtype=torch.int32, device=dev)
                 ctx.ko_res = open_setup(_header_arena(hdr_in), kidx_r, sks, pks, err)
+                if comm.world == 1 and ctx.led == list(live):
+                    ctx.res_in = ctx.res_arena  # one rank: the results are opened where they were sealed
             ctx.ev = torch.cuda.Event()
             ctx.ev.record(side)
         for t in (ctx.ks_res, ctx.ko_res):
@@ -156,8 +158,9 @@ class DeviceCommittee:
     def participate_exchange_clerk(self, secrets: torch.Tensor, live, err, owner_base: int = 0,
                                    marks=None):
         """Returns (acc, mask_arena): acc[c] = int64 [B] sum of clerk c's shares
-        over the boxes this rank opened (its hosted, live clerks), mask_arena =
-        this rank's participants' mask boxes sealed for the recipient (or None)."""
+        over the boxes this rank opened (zero for clerks it does not play),
+        mask_arena = this rank's participants' mask boxes sealed for the
+        recipient (or None)."""
         eng, comm = self.engine, self.comm
         spec, n, m = eng.spec, eng.n, eng.m
         W, me = comm.world, comm.rank
@@ -236,7 +239,9 @@ class DeviceCommittee:
             t.record_stream(side)
         eng._mark(marks, "keys")
 
-        acc: Dict[int, torch.Tensor] = {}
+        # running sums of the hosted clerks' shares: one int64 row per clerk (waves of
+        # sums below m never overflow), rows of clerks this rank does not play stay zero
+        acc = torch.zeros(n, B, dtype=torch.int64, device=dev)
         src2d = arena.ct.view(arena.M, arena.stride)
         dst2d = inbox.ct.view(inbox.M, inbox.stride)
         src_len, dst_len = arena.pt_len.view(-1, 1), inbox.pt_len.view(-1, 1)
@@ -257,20 +262,19 @@ class DeviceCommittee:
                 out = torch.empty(len(segs), B, dtype=torch.int32, device=dev)
                 open_sum(inbox.slice(base + first, rows), ko.slice(base + first, rows), err,
                          rows=len(segs), out=out)
-                parts = [(s.clerk, out[j]) for j, (_, s) in enumerate(segs)]
+                c0 = segs[0][1].clerk  # side-by-side segments are consecutive clerks
+                if [s.clerk for _, s in segs] == list(range(c0, c0 + len(segs))):
+                    acc[c0:c0 + len(segs)] += out
+                else:
+                    for j, (_, s) in enumerate(segs):
+                        acc[s.clerk] += out[j]
             else:
-                parts = []
                 for i, s in segs:
                     first, rows = pl.segment_rows(i)
                     out = torch.empty(B, dtype=torch.int32, device=dev)
                     open_sum(inbox.slice(base + first, rows), ko.slice(base + first, rows), err,
                              rows=1, out=out)
-                    parts.append((s.clerk, out))
-            for c, v in parts:
-                if c in acc:
-                    acc[c] += v  # int64: waves of sums below m never overflow
-                else:
-                    acc[c] = v.to(torch.int64)
+                    acc[s.clerk] += out
 
         pending = None
         G.gate_wait(gate)
@@ -335,7 +339,7 @@ class DeviceCommittee:
         if self.fault_hook is not None:
             self.fault_hook(stage, self.comm.rank)
 
-    def finish(self, ctx: RoundContext, acc: Dict[int, torch.Tensor], err, marks=None):
+    def finish(self, ctx: RoundContext, acc: torch.Tensor, err, marks=None):
         """Clerk-internal reduce, sealed results to the recipient, reveal.
         Returns (output or None, clerks_used)."""
         eng, comm = self.engine, self.comm
@@ -344,15 +348,8 @@ class DeviceCommittee:
         topic = f"r{ctx.rid}"
         ft = self.fault_tolerant and W > 1
         wire_dtype = torch.int32 if self._narrow else torch.int64
-        zero = None
-
-        def partial(c):
-            nonlocal zero
-            if c in acc:
-                return torch.remainder(acc[c], m).to(wire_dtype)
-            if zero is None:  # a host whose slice of the clerk is empty
-                zero = torch.zeros(B, dtype=wire_dtype, device=dev)
-            return zero
+        rem = torch.remainder(acc, m)  # [n][B] int64, canonical
+        wire = rem if wire_dtype == torch.int64 or W == 1 else rem.to(wire_dtype)
 
         # ---- clerk-internal: co-hosts' partial sums -> the clerk's lead
         self._hook("before_partials")
@@ -370,7 +367,7 @@ class DeviceCommittee:
                     inbound[c].append(buf)
                     comm.note("partial", "recv", r, c, buf.numel() * buf.element_size())
             elif c in go:
-                t = partial(c)
+                t = wire[c]
                 sends.append((hs[0], t))
                 comm.note("partial", "send", hs[0], c, t.numel() * t.element_size())
         comm.exchange_async(sends, recvs).wait()
@@ -381,12 +378,17 @@ class DeviceCommittee:
         torch.cuda.current_stream(dev).wait_event(ctx.ev)
         led_ok = [c for c in ctx.led if c in complete]
         if ctx.led:
-            combined = torch.zeros(len(ctx.led), B, dtype=torch.int32, device=dev)
-            for c in led_ok:
-                tot = partial(c).to(torch.int64)
-                for buf in inbound[c]:
-                    tot = tot + buf
-                combined[ctx.led.index(c)] = torch.remainder(tot, m).to(torch.int32)
+            lo, hi = ctx.led[0], ctx.led[-1] + 1
+            if led_ok == ctx.led and not any(inbound[c] for c in led_ok) and \
+                    ctx.led == list(range(lo, hi)):
+                combined = rem[lo:hi].to(torch.int32)  # no co-hosts: the sums are this rank's own
+            else:
+                combined = torch.zeros(len(ctx.led), B, dtype=torch.int32, device=dev)
+                for c in led_ok:
+                    tot = rem[c]
+                    for buf in inbound[c]:
+                        tot = tot + buf
+                    combined[ctx.led.index(c)] = torch.remainder(tot, m).to(torch.int32)
             eng.seal_results(ctx.res_arena, ctx.ks_res, combined, err)
         self._hook("before_results")
         arrived = result_stage(comm, topic, live, n, ft, led_ok, root)
@@ -403,8 +405,9 @@ class DeviceCommittee:
                     src = ctx.res_arena.ct.view(-1, ctx.res_arena.stride)[k:k + 1]
                     srcl = ctx.res_arena.pt_len.view(-1, 1)[k:k + 1]
                     if me == root:
-                        ctx.res_in.ct.view(-1, ctx.res_in.stride)[i:i + 1].copy_(src)
-                        ctx.res_in.pt_len.view(-1, 1)[i:i + 1].copy_(srcl)
+                        if ctx.res_in is not ctx.res_arena:
+                            ctx.res_in.ct.view(-1, ctx.res_in.stride)[i:i + 1].copy_(src)
+                            ctx.res_in.pt_len.view(-1, 1)[i:i + 1].copy_(srcl)
                     else:
                         sends += [(root, src), (root, srcl)]
                         comm.note("result", "send", root, c, src.numel())

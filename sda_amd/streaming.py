@@ -126,8 +126,8 @@ class StreamingAggregator:
                     ctx = committee.begin(live, err)
                     ctx.mask_acc = mask_acc
                 committee.ship_masks(ctx, mask_arena, err)
-                for c, v in part.items():
-                    acc[rows.index(c)] += v
+                for i, c in enumerate(rows):  # `part`: one row per clerk, this rank's are non-zero
+                    acc[i] += part[c]
                 mask_acc = ctx.mask_acc
             else:
                 comb, msum = eng.participate_and_clerk(x, live, err, owner_base=owner_base + first)
@@ -150,7 +150,10 @@ class StreamingAggregator:
             if ctx is None:  # resumed past the last wave
                 ctx = committee.begin(live, err)
                 ctx.mask_acc = mask_acc
-            out, used = committee.finish(ctx, {c: acc[i] for i, c in enumerate(rows)}, err, marks)
+            full = torch.zeros(eng.n, B, dtype=torch.int64, device=dev)
+            for i, c in enumerate(rows):
+                full[c] = acc[i]
+            out, used = committee.finish(ctx, full, err, marks)
             if check:
                 self._check(err)
             res = StreamResult(out, used, done, start)
