@@ -36,6 +36,9 @@ import os
 import sys
 import time
 
+# the host driver of the GPU boxes only supports dmabuf IPC (RCCL peer buffers)
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
@@ -183,15 +186,23 @@ def main():
         if rank == 0 and not torch.equal(res.output, expected):
             raise SystemExit(f"bench: {what}: aggregate does not match the reference sum")
 
-    # warmup: checked rounds (device error word + output)
+    # warmup: checked rounds (device error word + output). They run every device op of
+    # the timed loop too: the first use of an op in a process loads its code object,
+    # which on a machine that has not run the program before reads it from disk
+    # (tens of ms, measured: a first process timed 17 ms rounds, every later one 13.6)
+    err_total = torch.zeros(1, dtype=torch.int32, device="cuda")
     for i in range(args.warmup):
-        verify(agg.run_round(secrets, check=True), f"warmup round {i}")
+        res = agg.run_round(secrets, check=True)
+        err_total |= res.err
+        verify(res, f"warmup round {i}")
+    if args.warmup == 0:
+        err_total |= err_total
     if dist_mode:
         comm.reset_audit()
         comm.barrier()
+    err_total.zero_()
     torch.cuda.synchronize()
     torch.cuda.reset_peak_memory_stats()
-    err_total = torch.zeros(1, dtype=torch.int32, device="cuda")
     res = None
     t0 = time.perf_counter()
     for i in range(args.steps):
