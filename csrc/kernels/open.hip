@@ -64,8 +64,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   const uint64_t tmask = traw & byte_range_mask(lo, hi);
   uint32_t total;
   const uint32_t local = block_excl_scan((uint32_t)__popcll(tmask), scratch, &total);  // syncs
-  uint32_t prev_word = __shfl_up(w[15], 1, 64);
-  if ((tid & 63) == 0) prev_word = wave_prev;
+  const uint32_t prev_word = wave_shift_up1(w[15], wave_prev);  // lane 0: from global
   StageSink<VT> sink{outb, (uint32_t)(kChunkBytes + 2 * (tid & 63))};
   bool bad = decode_lane<sizeof(VT) == 2>(w, prev_word, tmask, traw, local, mp, gmsg, p0, sink);
   // a message must end on a terminator
@@ -179,9 +178,8 @@ SDA_DEV void decode_sum_body(uint32_t* acc, uint32_t (*info)[4], int L, int P, i
         const uint64_t tmask = traw & byte_range_mask(lo, hi);
         const uint32_t c = (uint32_t)__popcll(tmask);
         const uint32_t incl = wave_incl_scan(c);
-        const uint32_t total = __shfl(incl, 63, 64);
-        uint32_t prev_word = __shfl_up(w[15], 1, 64);
-        if (lane == 0) prev_word = wave_prev;
+        const uint32_t total = wave_read_lane(incl, 63);
+        const uint32_t prev_word = wave_shift_up1(w[15], wave_prev);  // lane 0: from global
         Sink sink{acc, rank + kSumMargin - E0};
         bad |= decode_lane<kFast16>(w, prev_word, tmask, traw, incl - c, mp, gmsg, p0, sink);
         if (hi > lo && p0 + hi == N && (gmsg[N - 1] & 0x80)) bad = true;
@@ -324,8 +322,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
       if (n_valid) fetch_next();
       {
         const int64_t p0 = c0 + 64 * lane;
-        uint32_t pm1 = __shfl_up(w[15], 1, 64);  // the 4 bytes before this lane's (raw)
-        if (lane == 0) pm1 = wave_prev;
+        // the 4 bytes before this lane's (raw; lane 0's come from global memory)
+        uint32_t pm1 = wave_shift_up1(w[15], wave_prev);
         const int lo = (int)max((int64_t)0, qs - p0);
         const int hi = (int)min((int64_t)64, qe - p0);
         // a message must end on a terminator
@@ -367,7 +365,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
           bad |= (pm1 >> 16) & (pm1 >> 24) & 0x80u;             // two continuation bytes before it
         }
         const uint32_t incl = wave_incl_scan(c);
-        const uint32_t total = __shfl(incl, 63, 64);
+        const uint32_t total = wave_read_lane(incl, 63);
         // byte offset (within acc) of the rank of this lane's first terminator
         uint32_t a4 = 4u * (rank + kSumMargin - E0 + (incl - c));
         lds_add(acc, a4, ((pm1 >> 24) & 0x7fu) & (0u - (pm1 >> 31)));

@@ -676,11 +676,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         }
         cnt = (uint32_t)__popcll(tmask & vmask);
       }
-      if (sub_cnt) {  // per 1 KiB sub-chunk: the 16 lanes covering it
-        uint32_t sc = cnt;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) sc += __shfl_xor(sc, o, 64);
-        if ((tid & 15) == 0) sub_cnt[((size_t)j * K + k) * kSubPerChunk + (tid >> 4)] = sc;
+      if (sub_cnt) {  // per 1 KiB sub-chunk: the 16 lanes covering it (sum on the last one)
+        const uint32_t sc = row16_incl_scan(cnt);
+        if ((tid & 15) == 15) sub_cnt[((size_t)j * K + k) * kSubPerChunk + (tid >> 4)] = sc;
       }
       if (term_cnt) {
         const uint32_t tot = block_sum(cnt, scratch);
