@@ -29,13 +29,21 @@ constexpr int kValuesPerLane = kEncodeValues / kBlock;  // 32
 // Index of a message's last chunk (chunk k covers message bytes [kC - 32, (k+1)C - 32)).
 SDA_DEV int last_chunk(uint32_t N) { return (int)(((int64_t)N + 31) / kChunkBytes); }
 
+// 16 bytes from an address that is only aligned to the value type: message rows
+// start at j * L values, which is 16-byte aligned only for some L. The target's
+// unaligned access mode (the HSA default) lets this be one global_load_dwordx4.
+struct __attribute__((packed, aligned(1))) Vec16 {
+  uint4 v;
+};
+
 template <typename VT>
-SDA_DEV void load_values(uint32_t (&v)[kValuesPerLane], const VT* src, int e0, int L, bool vec_ok) {
-  if (vec_ok && e0 + kValuesPerLane <= L) {
+SDA_DEV void load_values(uint32_t (&v)[kValuesPerLane], const VT* src, int e0, int L) {
+  if (e0 + kValuesPerLane <= L) {
+    const Vec16* p = reinterpret_cast<const Vec16*>(src + e0);
     if constexpr (sizeof(VT) == 1) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const uint4 d = reinterpret_cast<const uint4*>(src + e0)[q];
+        const uint4 d = p[q].v;
         const uint32_t ws[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -46,7 +54,7 @@ SDA_DEV void load_values(uint32_t (&v)[kValuesPerLane], const VT* src, int e0, i
     } else if constexpr (sizeof(VT) == 2) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const uint4 d = reinterpret_cast<const uint4*>(src + e0)[q];
+        const uint4 d = p[q].v;
         const uint32_t ws[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -57,7 +65,7 @@ SDA_DEV void load_values(uint32_t (&v)[kValuesPerLane], const VT* src, int e0, i
     } else {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const uint4 d = reinterpret_cast<const uint4*>(src + e0)[q];
+        const uint4 d = p[q].v;
         v[4 * q] = d.x; v[4 * q + 1] = d.y; v[4 * q + 2] = d.z; v[4 * q + 3] = d.w;
       }
     }
@@ -105,9 +113,8 @@ __global__ void __launch_bounds__(kBlock)
   const int tid = threadIdx.x;
   const int e0 = t * kEncodeValues + tid * kValuesPerLane;
   const VT* src = vals + (size_t)j * L;
-  const bool vec_ok = ((size_t)L * sizeof(VT)) % 16 == 0;
   uint32_t v[kValuesPerLane];
-  load_values<VT>(v, src, e0, L, vec_ok);
+  load_values<VT>(v, src, e0, L);
   // Fast lanes (all 32 values present and < 2^13, i.e. 1- or 2-byte varints):
   // branch-free encode, each value stores both candidate bytes and the next
   // value overwrites the second one when the varint was a single byte (same
