@@ -10,6 +10,7 @@
 
 #include "device_crypto.hpp"
 #include "kernels.hpp"
+#include "modarith.hpp"
 #include "sda/crypto.hpp"
 
 using namespace sdagpu;
@@ -480,6 +481,25 @@ int main() {
       bytes(dtb, dt, 4);
       CHECK(std::memcmp(tag, dtb, 16) == 0, "poly1305 fused tiles N=%u it=%d", N, it);
     }
+  }
+  // 7. the 24-bit Barrett reduction of the small-field share kernel: exhaustive over
+  //    every sum it can see, for each modulus the parameter search accepts
+  {
+    int accepted = 0;
+    for (uint32_t m : {2u, 3u, 13u, 101u, 241u, 251u, 257u, 433u, 521u, 769u, 1009u, 4093u, 8191u}) {
+      for (int terms : {5, 7}) {
+        const uint64_t wmax = (uint64_t)terms * (m - 1) * (m - 1);
+        const Mod24 P = make_mod24(m, wmax);
+        if (!P.c) continue;
+        ++accepted;
+        bool ok = true;
+        for (uint64_t w = 0; w <= wmax && ok; ++w) ok = mod24((uint32_t)w, P) == (uint32_t)(w % m);
+        CHECK(ok, "mod24 m=%u terms=%d (k=%u c=%u)", m, terms, P.k, P.c);
+      }
+    }
+    CHECK(accepted >= 10, "mod24 parameter search accepted only %d cases", accepted);
+    CHECK(make_mod24(433, 7ull * 432 * 432).c != 0 && make_mod24(241, 5ull * 240 * 240).c != 0,
+          "mod24 must cover the benchmark fields");
   }
   std::printf(failures ? "host_emul: %d FAILURES\n" : "host_emul: all ok\n", failures);
   return failures ? 1 : 0;

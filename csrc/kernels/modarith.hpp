@@ -38,6 +38,26 @@ SDA_DEV uint32_t mod32(uint32_t w, const ModParams& P) {
   uint32_t r = w - q * P.m;
   return r >= P.m ? r - P.m : r;
 }
+// Exact reduction of small sums on the full-rate 24-bit multipliers (mod32's 32-bit
+// multiplies run at a quarter of the rate): for w <= wmax,
+//   q = ((w << k) * c) >> 32 = floor(w / m),  c = ceil(2^(32 - k) / m),
+// whenever c < 2^24, (wmax << k) < 2^24 and wmax * m < 2^(32 - k) (then the excess
+// of c over 2^(32-k)/m, below 1, moves w c / 2^(32-k) by less than 1/m).
+struct Mod24 {
+  uint32_t k, c, m;  // c == 0: no valid (k, c) for this modulus and bound
+};
+inline Mod24 make_mod24(uint32_t m, uint64_t wmax) {
+  for (uint32_t k = 0; k <= 8; ++k) {
+    const uint64_t pw = 1ull << (32 - k);
+    const uint64_t c = (pw + m - 1) / m;
+    if (c < (1u << 24) && (wmax << k) < (1u << 24) && wmax * m < pw) return Mod24{k, (uint32_t)c, m};
+  }
+  return Mod24{0, 0, m};
+}
+SDA_DEV uint32_t mod24(uint32_t w, const Mod24& P) {
+  const uint32_t q = (uint32_t)(((uint64_t)((w << P.k) & 0xffffffu) * (uint64_t)(P.c & 0xffffffu)) >> 32);
+  return w - (q & 0xffffffu) * (P.m & 0xffffffu);  // q, m < 2^24: a 24-bit multiply-subtract
+}
 SDA_DEV uint32_t mod64(uint64_t v, const ModParams& P) {
   uint64_t q = __umul64hi(v, P.mu64);
   uint64_t r = v - q * (uint64_t)P.m;  // q >= floor(v/m) - 2

@@ -823,26 +823,30 @@ __global__ void __launch_bounds__(kBlock)
 // come from one ChaCha block as Lemire triples (11 of its 16 words; rejected
 // words are replaced by its other 5, then by the per-word retry stream) --
 // where k_share_pss spends a whole block on every batch. Thread i of block b
-// handles batches b * 4096 + i + 256 g, g < 16 (count tile b; consecutive lanes
-// store consecutive u16 shares). M is staged in LDS with rows padded to 8, read
-// as two broadcast 16-byte loads per clerk.
+// handles 16 batches of count tile b in runs of 4 / sizeof(share) adjacent ones
+// (consecutive lanes store consecutive 32-bit words of shares). M is read through
+// scalar loads (its addresses are uniform) and multiplied from SGPRs.
+struct __attribute__((packed, aligned(1))) Word32 {
+  uint32_t v;
+};
+struct __attribute__((packed, aligned(4))) Words2 {
+  uint2 v;
+};
 constexpr int kPssKS = 3;  // secrets per batch
 constexpr int kPssNC = 8;  // clerks
 
-template <int T, typename VT>
-__global__ void __launch_bounds__(kBlock)
-    k_share_pss48(int P, int D, ModParams mp, uint32_t m3, uint32_t t3,
+template <int T, typename VT, bool kMod24>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(T == 4 ? 3 : 2)))
+    k_share_pss48(int P, int D, ModParams mp, Mod24 m24, uint32_t m3, uint32_t t3,
                   const int32_t* __restrict__ secrets, const uint32_t* __restrict__ mat,
                   RngKeyArg rng, uint64_t owner_base, VT* __restrict__ shares,
                   uint32_t* __restrict__ cnt) {
   constexpr int K = kPssKS + T;
   constexpr int kPerBlock = 32 / T;      // batches per ChaCha block
+  constexpr int kAdj = 4 / sizeof(VT);   // adjacent batches per thread: one 32-bit store per clerk
   constexpr int kRounds = 16 / kPerBlock;
-  __shared__ __attribute__((aligned(16))) uint32_t sM[kPssNC][8];
   __shared__ uint32_t partial[kPssNC][kWaves];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  if (tid < kPssNC * 8) sM[tid >> 3][tid & 7] = (tid & 7) < K ? mat[(tid >> 3) * K + (tid & 7)] : 0u;
-  __syncthreads();
   const int tile = blockIdx.x, p = blockIdx.y, Tt = gridDim.x;
   const int B = (D + kPssKS - 1) / kPssKS;
   const uint64_t owner = owner_base + (uint64_t)p;
@@ -855,6 +859,30 @@ __global__ void __launch_bounds__(kBlock)
 
 #pragma unroll 1
   for (int rd = 0; rd < kRounds; ++rd) {
+    // this round's batches. A thread takes runs of kAdj adjacent batches (4 bytes of
+    // shares per clerk), so that a run's shares leave in one 32-bit store and its
+    // secrets arrive as consecutive words -- requested here, ahead of the ChaCha
+    // block, which covers their latency.
+    int32_t raw[kPerBlock * kPssKS];
+#pragma unroll
+    for (int q = 0; q < kPerBlock / kAdj; ++q) {
+      const int b0 = tile * kTileValues + kAdj * (tid + kBlock * (rd * (kPerBlock / kAdj) + q));
+      const int32_t* src = reinterpret_cast<const int32_t*>(
+          reinterpret_cast<const char*>(secrets + (size_t)p * D) + (uint32_t)b0 * (uint32_t)(kPssKS * 4));
+      int32_t* dst = raw + q * kAdj * kPssKS;
+      if ((b0 + kAdj) * kPssKS <= D) {  // the run's secrets are all there: consecutive words
+        const Words2* v = reinterpret_cast<const Words2*>(src);
+#pragma unroll
+        for (int i = 0; i < kAdj * kPssKS / 2; ++i) {
+          const uint2 d = v[i].v;
+          dst[2 * i] = (int32_t)d.x;
+          dst[2 * i + 1] = (int32_t)d.y;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kAdj * kPssKS; ++i) dst[i] = b0 * kPssKS + i < D ? src[i] : 0;
+      }
+    }
     uint32_t w[16];
     const uint64_t ctr = ((uint64_t)tile * kBlock + tid) * kRounds + rd;
     rng_block(w, rk, stream_id(kPurposeSharesPss48, owner), ctr);
@@ -889,39 +917,53 @@ __global__ void __launch_bounds__(kBlock)
       dg[3 * i + 1] = __umulhi(x1, m);
       dg[3 * i + 2] = __umulhi(x1 * m, m);
     }
-    // this round's batches: secrets (canonical) and randomness
+    // secrets (canonical) of this round's batches
     uint32_t s[kPerBlock][kPssKS];
     bool ok[kPerBlock];
-    int bidx[kPerBlock];
+    // batch indices as unsigned 32-bit offsets from the clerk's (uniform) row pointer:
+    // one address register per run instead of a 64-bit pair per (clerk, run)
+    uint32_t bidx[kPerBlock];
 #pragma unroll
     for (int g = 0; g < kPerBlock; ++g) {
-      const int b = tile * kTileValues + tid + kBlock * (rd * kPerBlock + g);
-      bidx[g] = b;
-      ok[g] = b < B;
+      const int q = g / kAdj, a = g % kAdj;
+      bidx[g] = (uint32_t)(tile * kTileValues + kAdj * (tid + kBlock * (rd * (kPerBlock / kAdj) + q)) + a);
+      ok[g] = bidx[g] < (uint32_t)B;
 #pragma unroll
-      for (int j = 0; j < kPssKS; ++j) {
-        const int e = b * kPssKS + j;
-        s[g][j] = (ok[g] && e < D) ? canon_i32(secrets[(size_t)p * D + e], mp) : 0u;
-      }
+      for (int j = 0; j < kPssKS; ++j) s[g][j] = canon_i32(raw[g * kPssKS + j], mp);
       nvalid += ok[g] ? 1u : 0u;
     }
 #pragma unroll
     for (int c = 0; c < kPssNC; ++c) {
-      const uint4 m0 = *reinterpret_cast<const uint4*>(&sM[c][0]);
-      const uint4 m1 = *reinterpret_cast<const uint4*>(&sM[c][4]);
-      const uint32_t row[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+      // the clerk's row of M: uniform addresses, i.e. scalar loads into SGPRs (a VGPR
+      // copy of all 8 rows next to the 64 accumulators left 2 waves per SIMD)
+      uint32_t row[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) row[j] = mat[c * K + j];
       VT* out = shares + ((size_t)c * P + p) * B;
 #pragma unroll
-      for (int g = 0; g < kPerBlock; ++g) {
-        uint32_t acc = 0;
+      for (int q = 0; q < kPerBlock / kAdj; ++q) {
+        uint32_t y[kAdj];
 #pragma unroll
-        for (int j = 0; j < kPssKS; ++j) acc += __umul24(row[j], s[g][j]);
+        for (int a = 0; a < kAdj; ++a) {
+          const int g = q * kAdj + a;
+          uint32_t acc = 0;
 #pragma unroll
-        for (int d = 0; d < T; ++d) acc += __umul24(row[kPssKS + d], dg[g * T + d]);
-        const uint32_t y = mod32(acc, mp);
-        if (ok[g]) {
-          out[bidx[g]] = (VT)y;
-          extra[c] += y >= 64u ? 1u : 0u;
+          for (int j = 0; j < kPssKS; ++j) acc += __umul24(row[j], s[g][j]);
+#pragma unroll
+          for (int d = 0; d < T; ++d) acc += __umul24(row[kPssKS + d], dg[g * T + d]);
+          y[a] = kMod24 ? mod24(acc, m24) : mod32(acc, mp);
+          extra[c] += (ok[g] && y[a] >= 64u) ? 1u : 0u;
+        }
+        if (ok[q * kAdj + kAdj - 1]) {  // the whole run lies inside the row
+          uint32_t word = 0;
+#pragma unroll
+          for (int a = 0; a < kAdj; ++a) word |= y[a] << (8 * sizeof(VT) * a);
+          // (row starts are only VT-aligned)
+          reinterpret_cast<Word32*>(reinterpret_cast<char*>(out) + bidx[q * kAdj] * (uint32_t)sizeof(VT))->v = word;
+        } else {
+#pragma unroll
+          for (int a = 0; a < kAdj; ++a)
+            if (ok[q * kAdj + a]) out[bidx[q * kAdj + a]] = (VT)y[a];
         }
       }
     }
@@ -1082,9 +1124,19 @@ void launch_share_pss(int P, int D, int n, int k, int t, uint32_t p, int value_b
   if (g_pss48 && value_bytes <= 2 && mask_mode == kMaskNone && k == kPssKS && n == kPssNC &&
       (t == 2 || t == 4) && p <= 8192u && p3 < (1ull << 32)) {
     const uint32_t t3 = (uint32_t)((1ull << 32) % p3);
+    // a share is a sum of k + t products of canonical values
+    const Mod24 m24 = make_mod24(p, (uint64_t)(k + t) * (p - 1) * (p - 1));
 #define SDA_PSS48(TT, VT)                                                                     \
-  hipLaunchKernelGGL((k_share_pss48<TT, VT>), grid, dim3(kBlock), 0, s, P, D, mp, (uint32_t)p3, \
-                     t3, secrets, share_matrix, rng, owner_base, (VT*)shares, cnt)
+  do {                                                                                        \
+    if (m24.c)                                                                                \
+      hipLaunchKernelGGL((k_share_pss48<TT, VT, true>), grid, dim3(kBlock), 0, s, P, D, mp, m24, \
+                         (uint32_t)p3, t3, secrets, share_matrix, rng, owner_base, (VT*)shares,  \
+                         cnt);                                                                \
+    else                                                                                      \
+      hipLaunchKernelGGL((k_share_pss48<TT, VT, false>), grid, dim3(kBlock), 0, s, P, D, mp, m24, \
+                         (uint32_t)p3, t3, secrets, share_matrix, rng, owner_base, (VT*)shares,  \
+                         cnt);                                                                \
+  } while (0)
     if (value_bytes == 1) {  // p <= 256: a share per byte
       if (t == 4) SDA_PSS48(4, uint8_t); else SDA_PSS48(2, uint8_t);
     } else {
