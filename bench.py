@@ -90,13 +90,14 @@ def parse():
                     help="N > 1. committee (default): sealed boxes routed to the clerks' GPUs, "
                          "per-rank key custody, sealed results to rank 0. owner: non-private "
                          "upper bound, each GPU opens its own participants' boxes")
-    ap.add_argument("--waves", type=int, default=0,
+    ap.add_argument("--waves", type=lambda v: v if v == "taper" else int(v), default=0,
                     help="committee layout: participant waves the exchange is pipelined over. "
-                         "0 (default): with N > 1, 2 / 4 / 8 waves are timed for two untimed rounds "
-                         "each before the warm-up and the fastest is used (more waves start the "
-                         "all-to-all earlier and shorten the exposed last wave, fewer waves keep "
-                         "the grids large: which wins depends on the xGMI rate RCCL reaches); "
-                         "4 on a single rank")
+                         "A count, or 'taper' (six waves of 1/16, 3/16, 4/16, 4/16, 3/16, 1/16 of the "
+                         "participants). 0 (default): with N > 1, 2 / 4 / 8 / taper are timed for "
+                         "two untimed rounds each before the warm-up and the fastest is used (more "
+                         "waves start the all-to-all earlier and shorten the exposed last wave, "
+                         "fewer waves keep the grids large: which wins depends on the xGMI rate "
+                         "RCCL reaches); 4 on a single rank")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the distributed engine even on one rank (measures its overhead)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -156,16 +157,16 @@ def main():
     else:
         from sda_amd.parallel.engine import DistributedAggregator
 
-        waves = args.waves if args.waves > 0 else 4
+        waves = args.waves if args.waves else 4
         agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", dev_index),
                                     time_stages=args.stages, layout=args.layout,
                                     waves=waves, force_pipeline=args.force_dist,
                                     deadline_s=min(60.0, args.dist_timeout / 4))
         engine, comm = agg.engine, agg.comm
-        if args.waves <= 0 and world > 1 and args.layout == "committee":
+        if not args.waves and world > 1 and args.layout == "committee":
             # untimed: pick the pipeline depth on this node's measured exchange rate
             # (every rank takes the same decision: the times are max-reduced)
-            for w in (2, 4, 8):
+            for w in (2, 4, 8, "taper"):
                 agg.set_waves(w)
                 agg.run_round(secrets, check=True)
                 comm.barrier()

@@ -66,7 +66,7 @@ class DeviceCommittee:
     def __init__(self, engine: DeviceAggregator, comm: Comm, waves: int = 4,
                  force_pipeline: bool = False, fault_tolerant: bool = True, fault_hook=None):
         self.engine, self.comm = engine, comm
-        self.waves = max(1, waves)
+        self.set_waves(waves)
         self.force_pipeline = force_pipeline
         self.fault_tolerant = fault_tolerant
         self.fault_hook = fault_hook
@@ -81,6 +81,35 @@ class DeviceCommittee:
         self._rid = 0
         # int32 sums of `world` values below m are exact when they fit
         self._narrow = W * (engine.m - 1) < 2 ** 31
+
+    # ------------------------------------------------------------------ waves ----
+    TAPER = (1, 3, 4, 4, 3, 1)  # sixteenths of the participants per wave
+
+    def set_waves(self, waves) -> None:
+        """`waves`: a count (equal waves) or "taper": six waves of 1/16, 3/16, 4/16,
+        4/16, 3/16, 1/16 of the participants -- when the exchange is what bounds the
+        round, its critical path is the first wave's seal + all transfers + the last
+        wave's open, so small first and last waves shorten it without the small
+        grids of many equal waves."""
+        if waves == "taper":
+            self.waves = "taper"
+        else:
+            self.waves = max(1, int(waves))
+
+    def wave_bounds(self, P: int, pipelined: bool):
+        """Participant ranges [lo, hi) of the waves (the same on every rank)."""
+        if not pipelined:
+            return [(0, P)]
+        if self.waves == "taper":
+            cuts, acc = [0], 0
+            for f in self.TAPER:
+                acc += f
+                cuts.append(P * acc // 16)
+            bounds = list(zip(cuts, cuts[1:]))
+        else:
+            nw = min(self.waves, P)
+            bounds = [(P * w // nw, P * (w + 1) // nw) for w in range(nw)]
+        return [(lo, hi) for lo, hi in bounds if hi > lo]
 
     # ------------------------------------------------------------------ begin ----
     def begin(self, live, err) -> RoundContext:
@@ -172,9 +201,7 @@ class DeviceCommittee:
         secrets = secrets.contiguous()
         P, D = secrets.shape
         B, dev = spec.batches, eng.device
-        nw = min(self.waves, P) if (W > 1 or self.force_pipeline) else 1
-        bounds = [(P * w // nw, P * (w + 1) // nw) for w in range(nw)]
-        bounds = [(lo, hi) for lo, hi in bounds if hi > lo]
+        bounds = self.wave_bounds(P, W > 1 or self.force_pipeline)
         plans = [plan(me, W, n, hi - lo) for lo, hi in bounds]
         routers = [RowRouter(comm, pl) for pl in plans]
         in_base, rows_in = [], 0

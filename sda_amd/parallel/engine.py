@@ -100,12 +100,13 @@ class DistributedAggregator:
         self._narrow = self.world * (spec.field_modulus - 1) < 2 ** 31
         self._rid = 0
 
-    def set_waves(self, waves: int) -> None:
-        """Participant waves the committee exchange is pipelined over (takes
-        effect at the next round; every rank must use the same value)."""
+    def set_waves(self, waves) -> None:
+        """Participant waves the committee exchange is pipelined over: a count, or
+        "taper" (small first and last waves; see DeviceCommittee.set_waves). Takes
+        effect at the next round; every rank must use the same value."""
         cm = getattr(self, "_committee", None)
         if cm is not None:
-            cm.waves = max(1, int(waves))
+            cm.set_waves(waves)
 
     # ---- key custody -----------------------------------------------------------
     def _keys(self, n: int):
