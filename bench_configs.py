@@ -12,6 +12,7 @@ JSON line each (rank 0).
   --config 6  1k x 1M, the reference's PSS_155_728_100 (728 clerks) on the int8-limb
               MFMA GEMM
   --config 7  config 5 over a prime below 256 (u8 share storage)
+  --config 8  16 x 1M per GPU, the reference's PSS_155_19682_100 (19,682 clerks)
 
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench_configs.py --config 3
 Scaled-down runs: --participants / --dim override the per-rank sizes;
@@ -34,7 +35,7 @@ if ROOT not in sys.path:
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 3, 4, 5, 6, 7])
+    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 3, 4, 5, 6, 7, 8])
     ap.add_argument("--pss-backend", default=None, choices=["auto", "valu", "mfma"])
     ap.add_argument("--participants", type=int, default=None, help="per rank")
     ap.add_argument("--dim", type=int, default=None)

@@ -32,16 +32,68 @@ uint64_t mult_order(uint64_t w, uint64_t p, uint64_t limit) {
 
 namespace {
 
-// Lagrange basis value l_j(x) over nodes (mod p).
-uint64_t lagrange_basis(const std::vector<uint64_t>& nodes, size_t j, uint64_t x, uint64_t p) {
-  unsigned __int128 num = 1, den = 1;
-  for (size_t i = 0; i < nodes.size(); ++i) {
-    if (i == j) continue;
-    num = num * ((x + p - nodes[i]) % p) % p;
-    den = den * ((nodes[j] + p - nodes[i]) % p) % p;
+inline uint64_t mul(uint64_t a, uint64_t b, uint64_t p) { return (uint64_t)((unsigned __int128)a * b % p); }
+inline uint64_t sub(uint64_t a, uint64_t b, uint64_t p) { return a >= b ? a - b : a + p - b; }
+
+// v[i] <- 1 / v[i] for non-zero v[i] (one field inversion: Montgomery's trick).
+void batch_invert(std::vector<uint64_t>& v, uint64_t p) {
+  std::vector<uint64_t> pre(v.size() + 1, 1);
+  for (size_t i = 0; i < v.size(); ++i) pre[i + 1] = mul(pre[i], v[i], p);
+  uint64_t inv = mod_inv(pre[v.size()], p);
+  for (size_t i = v.size(); i-- > 0;) {
+    const uint64_t vi = v[i];
+    v[i] = mul(inv, pre[i], p);
+    inv = mul(inv, vi, p);
   }
-  return (uint64_t)(num * mod_inv((uint64_t)den, p) % p);
 }
+
+// Lagrange interpolation in barycentric form: l_j(x) = l(x) w_j / (x - x_j) with
+// l(x) = prod_i (x - x_i) and w_j = 1 / prod_{i != j} (x_j - x_i). The weights cost
+// O(N^2) multiplications once -- or O(N) when the nodes are all the N-th roots of
+// unity, where prod_{i != j} (x_j - x_i) = N x_j^(N-1) = N / x_j (the full share
+// point set {1, w_n, .., w_n^n} and the secret point set of the tss parameter sets)
+// -- and a row of basis values O(N). (Evaluating every l_j(x) by its own product,
+// as before, was O(N^2) per point: minutes for the 19,682-share set.)
+class Barycentric {
+ public:
+  Barycentric(std::vector<uint64_t> nodes, uint64_t p) : x_(std::move(nodes)), p_(p), w_(x_.size()) {
+    const size_t N = x_.size();
+    bool roots = N >= 2;
+    if (roots) {  // every node an N-th root of unity (they are distinct: validate())
+      for (size_t i = 0; i < N && roots; ++i) roots = mod_pow(x_[i], N, p) == 1;
+    }
+    if (roots) {
+      const uint64_t invN = mod_inv(N % p, p);
+      for (size_t j = 0; j < N; ++j) w_[j] = mul(x_[j], invN, p);
+    } else {
+      for (size_t j = 0; j < N; ++j) {
+        uint64_t d = 1;
+        for (size_t i = 0; i < N; ++i)
+          if (i != j) d = mul(d, sub(x_[j], x_[i], p), p);
+        w_[j] = d;
+      }
+      batch_invert(w_, p);
+    }
+  }
+  // out[j] = l_j(x) for every node j; x must not be a node.
+  void row(uint64_t x, std::vector<uint64_t>& out) const {
+    const size_t N = x_.size();
+    out.resize(N);
+    uint64_t l = 1;
+    for (size_t j = 0; j < N; ++j) {
+      out[j] = sub(x, x_[j], p_);
+      if (out[j] == 0) throw SdaError::invalid("packed shamir: evaluation point is a node");
+      l = mul(l, out[j], p_);
+    }
+    batch_invert(out, p_);
+    for (size_t j = 0; j < N; ++j) out[j] = mul(mul(l, w_[j], p_), out[j], p_);
+  }
+
+ private:
+  std::vector<uint64_t> x_;
+  uint64_t p_;
+  std::vector<uint64_t> w_;
+};
 
 }  // namespace
 
@@ -75,9 +127,11 @@ std::vector<uint32_t> PackedShamirParams::share_matrix() const {
   std::vector<uint64_t> nodes(K + 1);
   for (int j = 0; j <= K; ++j) nodes[j] = mod_pow(omega_secrets, j, p);
   std::vector<uint32_t> M((size_t)share_count * K);
+  const Barycentric basis(nodes, p);
+  std::vector<uint64_t> row;
   for (int c = 0; c < share_count; ++c) {
-    const uint64_t x = mod_pow(omega_shares, c + 1, p);
-    for (int j = 1; j <= K; ++j) M[(size_t)c * K + (j - 1)] = (uint32_t)lagrange_basis(nodes, j, x, p);
+    basis.row(mod_pow(omega_shares, c + 1, p), row);
+    for (int j = 1; j <= K; ++j) M[(size_t)c * K + (j - 1)] = (uint32_t)row[j];
   }
   return M;
 }
@@ -96,10 +150,11 @@ std::vector<uint32_t> PackedShamirParams::lagrange_matrix(const std::vector<int>
     nodes.push_back(mod_pow(omega_shares, i + 1, p));
   }
   std::vector<uint32_t> L((size_t)secret_count * indices.size());
+  const Barycentric basis(nodes, p);
+  std::vector<uint64_t> row;
   for (int s = 0; s < secret_count; ++s) {
-    const uint64_t x = mod_pow(omega_secrets, s + 1, p);
-    for (size_t i = 0; i < indices.size(); ++i)
-      L[(size_t)s * indices.size() + i] = (uint32_t)lagrange_basis(nodes, i + 1, x, p);
+    basis.row(mod_pow(omega_secrets, s + 1, p), row);
+    for (size_t i = 0; i < indices.size(); ++i) L[(size_t)s * indices.size() + i] = (uint32_t)row[i + 1];
   }
   return L;
 }

@@ -10,8 +10,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Callable, Optional, Sequence
 
-from .schemes import (PSS_4_8_3, PSS_155_728_100, Additive, AggregationSpec, NoMask, PackedShamir,
-                      pss_5_of_8)
+from .schemes import (PSS_4_8_3, PSS_155_728_100, PSS_155_19682_100, Additive, AggregationSpec,
+                      NoMask, PackedShamir, pss_5_of_8)
 
 
 @dataclass(frozen=True)
@@ -69,6 +69,10 @@ BENCH_CONFIGS = {
                     clerks=(0, 2, 3, 5, 7),
                     what="config 5 over a prime below 256: field elements stored as int8-sized "
                          "values (u8 shares)"),
+        BenchConfig(8, "pss155_19682_16x1m", 16, 1_000_000, lambda: PSS_155_19682_100,
+                    pss_backend="mfma",
+                    what="the reference's largest parameter set: 19,682 clerks, k=100, t=155 "
+                         "(315k sealed boxes of 10,000 shares for 16 participants per GPU)"),
     ]
 }
 

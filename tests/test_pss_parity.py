@@ -119,6 +119,21 @@ def test_large_set_dropout_reconstruct(native):
     assert [v % p for v in nat.reconstruct(idx, [shares[i] for i in idx])] == s
 
 
+def test_largest_set_reconstructs_from_all_and_from_survivors(native):
+    """PSS_155_19682_100 through the barycentric Lagrange matrices: every clerk
+    (node set = all 19,683rd roots of unity: the O(n) weight path), the bare
+    threshold, and a large survivor set (generic O(n^2) weights)."""
+    ps = PSS_155_19682_100
+    nat, p, n = ps.native(), ps.prime_modulus, ps.share_count
+    rng = random.Random(3)
+    s = [rng.randrange(p) for _ in range(ps.secret_count)]
+    r = [rng.randrange(p) for _ in range(ps.privacy_threshold_)]
+    shares = [v % p for v in nat.share(s, r)]
+    for idx in (list(range(n)), sorted(rng.sample(range(n), ps.reconstruction_threshold())),
+                [i for i in range(n) if i % 5]):
+        assert [v % p for v in nat.reconstruct(idx, [shares[i] for i in idx])] == s
+
+
 def test_reference_full_loop_vector(native):
     """full_loop.rs:57-64,148: two participants share [1,2,3,4] under PSS_4_8_3;
     the summed shares reconstruct to [2,4,6,8] (batches of 3, zero-padded)."""
