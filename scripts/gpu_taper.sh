@@ -9,4 +9,4 @@ for w in 4 taper; do
   echo "committee waves=$w $(tail -1 gpurun_out/rep_committee_w$w.log | grep -o '"ms_per_step": [0-9.]*')"
 done
 unset MASTER_ADDR MASTER_PORT RANK WORLD_SIZE LOCAL_RANK
-bash $R/scripts/gpu_bench_w2_gloo.sh | grep -o '"pipeline_wave.*timed_steps' 
+bash $R/scripts/gpu_bench_wN_gloo.sh 2
