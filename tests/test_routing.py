@@ -104,3 +104,25 @@ def test_plan_properties_random(world, n, P):
     assert len(got) == world * n * P
     for c in range(n):
         assert hosts(c, world, n)
+
+
+@pytest.mark.parametrize("waves", [1, 2, 4, 8, "taper"])
+@pytest.mark.parametrize("P", [1, 5, 16, 24, 250, 1000])
+def test_wave_bounds_cover_the_participants(waves, P):
+    """The pipelined committee round cuts a rank's participants into waves (equal
+    ones, or the tapered schedule with small first and last waves): consecutive,
+    non-empty ranges that cover [0, P) -- every rank derives the same cut."""
+    import types
+
+    from sda_amd.parallel.device_round import DeviceCommittee
+
+    me = types.SimpleNamespace(waves=waves, TAPER=DeviceCommittee.TAPER)
+    bounds = DeviceCommittee.wave_bounds(me, P, True)
+    assert bounds[0][0] == 0 and bounds[-1][1] == P
+    assert all(hi > lo for lo, hi in bounds)
+    assert all(a[1] == b[0] for a, b in zip(bounds, bounds[1:]))
+    assert len(bounds) <= (6 if waves == "taper" else waves)
+    assert DeviceCommittee.wave_bounds(me, P, False) == [(0, P)]
+    if waves == "taper" and P >= 16:
+        sizes = [hi - lo for lo, hi in bounds]
+        assert sizes[0] <= sizes[2] and sizes[-1] <= sizes[-3]
