@@ -1,7 +1,7 @@
 // VALU throughput micro-benchmark (gfx950): wave-instructions per cycle per CU
 // for the integer ops the SDA kernels lean on. Each thread runs 8 independent
 // chains of one op; enough waves to fill every SIMD.
-//   hipcc -O3 --offload-arch=gfx950 scripts/ubench_valu.hip -o /tmp/ubench && /tmp/ubench
+//   hipcc -O3 --offload-arch=gfx950 -Xclang -target-feature -Xclang -packed-fp32-ops scripts/ubench_valu.hip -o /tmp/ubench && /tmp/ubench
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
