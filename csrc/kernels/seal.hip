@@ -538,6 +538,42 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+// out[q][u] = word 4 i + u of the 16-word block `w` held by lane q of this lane's
+// quad, i = this lane's position in the quad: a 4 x 4 transpose of 4-word groups
+// over the quad's lanes in two butterfly steps (lane ^ 1, then lane ^ 2), moved by
+// DPP quad permutes. After step 1 slot s holds group (s & 2) | (i & 1) of lane
+// (i & 2) | (s & 1); step 2 exchanges slot pairs with lane ^ 2.
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xf, 0xf, true);
+}
+__device__ __forceinline__ void quad_transpose(uint32_t (&out)[4][4], const uint32_t (&w)[16], int lane) {
+  constexpr int kSwap1 = 0xB1;  // quad_perm [1, 0, 3, 2]
+  constexpr int kSwap2 = 0x4E;  // quad_perm [2, 3, 0, 1]
+  const bool odd = lane & 1, hi = lane & 2;
+  uint32_t a[4][4];
+#pragma unroll
+  for (int gp = 0; gp < 4; gp += 2) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t g0 = w[4 * gp + u], g1 = w[4 * (gp + 1) + u];
+      const uint32_t p0 = quad_perm<kSwap1>(g0), p1 = quad_perm<kSwap1>(g1);  // the partner's
+      a[gp][u] = odd ? p1 : g0;
+      a[gp + 1][u] = odd ? g1 : p0;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t lo_ = a[s][u], hi_ = a[s + 2][u];
+      const uint32_t plo = quad_perm<kSwap2>(lo_), phi = quad_perm<kSwap2>(hi_);
+      out[s][u] = hi ? phi : lo_;
+      out[s + 2][u] = hi ? hi_ : plo;
+    }
+  }
+}
+
 // Middle chunks on the matrix cores (+ in-place decryption and terminator
 // counts for every chunk when DECRYPT). A middle chunk (not the message's
 // first or last) is 1024 full blocks starting at block fb = kC/16 - 2, taken as
@@ -546,7 +582,8 @@ __global__ void __launch_bounds__(kBlock)
 // (wave w takes t in [16 w, 16 w + 16) of every row) and N = the 19 weight
 // digits (two 16-column tiles). Row i is then placed by r^(16 - i). First / last
 // chunks are k_mac_horner's (launched first: it reads the ciphertext this kernel
-// decrypts in place).
+// decrypts in place). With this K split wave w's operand bytes are exactly the
+// quarter [4096 w, 4096 (w + 1)) of the chunk.
 template <int DECRYPT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
     k_mac_chunks(int K, const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
@@ -597,106 +634,98 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         sub_cnt[((size_t)j * K + k) * kSubPerChunk + tid] = 0;
       continue;
     }
-    // Decrypt side: this lane's 64 bytes = keystream block kC/64 + tid, i.e.
-    // message bytes [kC - 32 + 64 tid, +64) (16-byte pieces overlapping
-    // [start, end); the MAC loads below hit the same lines in cache).
-    uint4 pt4[4];
-    if constexpr (DECRYPT) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t pos = kC - 32 + 64 * tid + 16 * q;
-        pt4[q] = make_uint4(0, 0, 0, 0);
-        if (pos >= start - 15 && pos >= 0 && pos < end) pt4[q] = *reinterpret_cast<const uint4*>(gmsg + pos);
-      }
-    }
+    // This lane's four 16-byte pieces of the chunk: piece q = keystream bytes
+    // [4096 wave + 1024 q + 16 lane, +16) of the chunk, so that a wave's load (and
+    // store) instruction covers 1 KiB contiguously -- a lane reading its own 64
+    // contiguous bytes made every instruction touch 64 lines and every store a
+    // 16-byte partial line write (350 M write requests per headline round; the
+    // memory side alone then took 3.1 ms against 2.4 ms in this layout). The
+    // pieces are also exactly this lane's MFMA operand fragments of the
+    // interleaved rows (row = lane & 15, t = 16 wave + 4 q + (lane >> 4)): one load
+    // serves the MAC and the decryption, and a wave reads only bytes it overwrites
+    // itself, so the in-place decryption needs no barrier.
     const bool middle = use_mfma && k != 0 && k != last;
-    v4i a[4];
-    if (middle) {
-      // row `row` = blocks row + 16 t of the chunk: 16 lanes read 256 contiguous bytes
-      const int64_t fb = kC / 16 - 2;
+    uint4 d4[4];
+    int64_t pos[4];
+    bool in[4];
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq)
-        a[qq] = *reinterpret_cast<const v4i*>(gmsg + 16 * (fb + row + 16 * (4 * (4 * wave + qq) + g)));
+    for (int q = 0; q < 4; ++q) {
+      pos[q] = kC - 32 + 4096 * wave + 1024 * q + 16 * lane;
+      in[q] = pos[q] >= start - 15 && pos[q] >= 0 && pos[q] < end;
+      d4[q] = make_uint4(0, 0, 0, 0);
+      if ((DECRYPT || middle) && in[q]) d4[q] = *reinterpret_cast<const uint4*>(gmsg + pos[q]);
     }
     // The keystream needs no loaded byte: computed here, its ~1000 instructions
-    // run while the chunk's loads (issued above) are in flight.
+    // run while the chunk's loads (issued above) are in flight. Lane 4 j + i of a
+    // wave computes block 16 i + j of the wave's 64: the four lanes of a quad hold
+    // the four blocks their pieces lie in (piece q in block 16 q + j, words 4 i ..).
     uint32_t w[16];
-    bool ks = false;
     if constexpr (DECRYPT) {
-      const int64_t p0 = 64 * (kC / 64 + tid) - 32;
-      ks = p0 < end && p0 + 64 > start;
-      if (ks) {
-        const MsgKey key = keys[j];
-        salsa20_block(w, key.subkey, key.nonce[0], key.nonce[1], (uint64_t)(kC / 64 + tid));
-      }
+      const MsgKey key = keys[j];
+      const uint64_t blk = (uint64_t)(kC / 64) + 64 * wave + 16 * (lane & 3) + (lane >> 2);
+      salsa20_block(w, key.subkey, key.nonce[0], key.nonce[1], blk);
     }
     if (middle) {
       v4i acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
-        const v4i x = a[qq] ^ (int)0x80808080;  // bytes u -> u - 128 (signed)
+        const v4i a = {(int)d4[qq].x, (int)d4[qq].y, (int)d4[qq].z, (int)d4[qq].w};
+        const v4i x = a ^ (int)0x80808080;  // bytes u -> u - 128 (signed)
         acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, b0[qq], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, b1[qq], acc1, 0, 0, 0);
       }
-      // C[segment 4 g + i][digit row]: |sum| < 2^23 per wave, 2^25 over the four
+      // C[row 4 g + i][digit column]: |sum| < 2^23 per wave, 2^25 over the four
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         atomicAdd(&cacc[k - k0][4 * g + i][row], acc0[i]);
         if (row < kPolyDigits - 16) atomicAdd(&cacc[k - k0][4 * g + i][16 + row], acc1[i]);
       }
-      // every MAC read of the chunk is done before its in-place decryption
-      if constexpr (DECRYPT) __syncthreads();
     }
 
     if constexpr (DECRYPT) {
-      // keystream block b covers message bytes [64b-32, 64b+32)
-      const int64_t b = kC / 64 + tid;
-      const int64_t p0 = 64 * b - 32;
-      if (ks) {
+      // 4 x 4 transpose of the keystream's word groups within each quad (two
+      // butterfly steps on the VALU): afterwards ks[q] = words 4 i .. 4 i + 3 of the
+      // block of quad lane q, i.e. the keystream of piece q
+      uint32_t ks[4][4];
+      quad_transpose(ks, w, lane);
+      uint32_t cnt[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          pt4[u].x ^= w[4 * u]; pt4[u].y ^= w[4 * u + 1]; pt4[u].z ^= w[4 * u + 2]; pt4[u].w ^= w[4 * u + 3];
-        }
-      }
-      // terminators (MSB clear) among this lane's valid bytes
-      const int vlo = (int)max((int64_t)0, start - p0);
-      const int vhi = (int)min((int64_t)64, end - p0);
-      uint32_t cnt = 0;
-      if (vlo == 0 && vhi == 64) {  // whole lane inside the message: popcounts in place
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          cnt += (uint32_t)__popc(~pt4[q].x & 0x80808080u) + (uint32_t)__popc(~pt4[q].y & 0x80808080u) +
-                 (uint32_t)__popc(~pt4[q].z & 0x80808080u) + (uint32_t)__popc(~pt4[q].w & 0x80808080u);
-        }
-      } else if (vhi > vlo) {
-        const uint64_t vmask = (vhi >= 64 ? ~0ull : ((1ull << vhi) - 1)) & ~((1ull << vlo) - 1);
-        uint64_t tmask = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t ws[4] = {pt4[q].x, pt4[q].y, pt4[q].z, pt4[q].w};
+      for (int q = 0; q < 4; ++q) {
+        d4[q].x ^= ks[q][0]; d4[q].y ^= ks[q][1]; d4[q].z ^= ks[q][2]; d4[q].w ^= ks[q][3];
+        // terminators (MSB clear) among the piece's bytes inside the message
+        const int vlo = (int)max((int64_t)0, min((int64_t)16, start - pos[q]));
+        const int vhi = (int)max((int64_t)0, min((int64_t)16, end - pos[q]));
+        if (vlo == 0 && vhi == 16) {
+          cnt[q] = (uint32_t)__popc(~d4[q].x & 0x80808080u) + (uint32_t)__popc(~d4[q].y & 0x80808080u) +
+                   (uint32_t)__popc(~d4[q].z & 0x80808080u) + (uint32_t)__popc(~d4[q].w & 0x80808080u);
+        } else {
+          const uint32_t ws[4] = {d4[q].x, d4[q].y, d4[q].z, d4[q].w};
+          uint32_t tmask = 0;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const uint32_t t = ~ws[u] & 0x80808080u;
-            const uint64_t bits = ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
-            tmask |= bits << (16 * q + 4 * u);
+            tmask |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * u);
           }
+          const uint32_t vmask = vhi > vlo ? ((1u << vhi) - 1u) & ~((1u << vlo) - 1u) : 0u;
+          cnt[q] = (uint32_t)__popc(tmask & vmask);
         }
-        cnt = (uint32_t)__popcll(tmask & vmask);
       }
-      if (sub_cnt) {  // per 1 KiB sub-chunk: the 16 lanes covering it (sum on the last one)
-        const uint32_t sc = row16_incl_scan(cnt);
-        if ((tid & 15) == 15) sub_cnt[((size_t)j * K + k) * kSubPerChunk + (tid >> 4)] = sc;
+      if (sub_cnt) {  // per 1 KiB sub-chunk 4 wave + q: every lane's piece q
+        const uint32_t s01 = wave_read_lane(wave_incl_scan(cnt[0] | (cnt[1] << 16)), 63);
+        const uint32_t s23 = wave_read_lane(wave_incl_scan(cnt[2] | (cnt[3] << 16)), 63);
+        if (lane < 4) {
+          const uint32_t pair = lane < 2 ? s01 : s23;
+          sub_cnt[((size_t)j * K + k) * kSubPerChunk + 4 * wave + lane] = (lane & 1) ? pair >> 16 : pair & 0xffffu;
+        }
       }
       if (term_cnt) {
-        const uint32_t tot = block_sum(cnt, scratch);
+        const uint32_t tot = block_sum(cnt[0] + cnt[1] + cnt[2] + cnt[3], scratch);
         if (tid == 0) term_cnt[(size_t)j * K + k] = tot;
       }
       // store plaintext in place (bytes past `end` land in the slot padding)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t pos = p0 + 16 * q;
-        if (pos >= start - 15 && pos >= 0 && pos < end) *reinterpret_cast<uint4*>(gmsg + pos) = pt4[q];
-      }
+      for (int q = 0; q < 4; ++q)
+        if (in[q]) *reinterpret_cast<uint4*>(gmsg + pos[q]) = d4[q];
     }
   }
   if (!any_middle) return;
