@@ -113,24 +113,58 @@ __global__ void __launch_bounds__(kBlock)
   const int tid = threadIdx.x;
   const int e0 = t * kEncodeValues + tid * kValuesPerLane;
   const VT* src = vals + (size_t)j * L;
-  uint32_t v[kValuesPerLane];
-  load_values<VT>(v, src, e0, L);
-  // Fast lanes (all 32 values present and < 2^13, i.e. 1- or 2-byte varints):
-  // branch-free encode, each value stores both candidate bytes and the next
-  // value overwrites the second one when the varint was a single byte (same
-  // lane, so LDS program order holds). Other lanes take the generic path.
-  uint32_t orv = 0;
-#pragma unroll
-  for (int i = 0; i < kValuesPerLane; ++i) orv |= v[i];
-  const bool fast = (e0 + kValuesPerLane <= L) && orv < 8192u;
+  const bool full = e0 + kValuesPerLane <= L;
+  uint32_t v[kValuesPerLane];            // the lane's values (u8 / u32 storage)
+  uint32_t pr[kValuesPerLane / 2] = {};  // u16 storage: the lane's values as pairs, as loaded
+  // Fast lanes (all 32 values present and < 2^13, i.e. 1- or 2-byte varints of
+  // non-negative values) encode branch-free; other lanes take the generic path.
+  bool fast;
   uint32_t my_bytes = 0;
-  if (fast) {
+  if constexpr (sizeof(VT) == 2) {
+    // u16 pairs stay packed: both halves of a dword are handled by one
+    // instruction (v < 2^13, so no step carries from the low half into the high)
+    uint32_t orp = 0;
+    if (full) {
+      const Vec16* p = reinterpret_cast<const Vec16*>(src + e0);
 #pragma unroll
-    for (int i = 0; i < kValuesPerLane; ++i) my_bytes += 1u + (v[i] >= 64u);
+      for (int q = 0; q < 4; ++q) {
+        const uint4 d = p[q].v;
+        pr[4 * q] = d.x; pr[4 * q + 1] = d.y; pr[4 * q + 2] = d.z; pr[4 * q + 3] = d.w;
+      }
+#pragma unroll
+      for (int k = 0; k < kValuesPerLane / 2; ++k) orp |= pr[k];
+    } else {
+#pragma unroll
+      for (int i = 0; i < kValuesPerLane; ++i)
+        pr[i >> 1] |= ((e0 + i < L) ? (uint32_t)src[e0 + i] : 0u) << (16 * (i & 1));
+    }
+    fast = full && (orp & 0xe000e000u) == 0u;
+    if (fast) {
+      my_bytes = kValuesPerLane;  // + one per value >= 64 (bit 15 of half + 0x7fc0)
+#pragma unroll
+      for (int k = 0; k < kValuesPerLane / 2; ++k)
+        my_bytes += (uint32_t)__popc((pr[k] + 0x7fc07fc0u) & 0x80008000u);
+    }
   } else {
+    load_values<VT>(v, src, e0, L);
+    uint32_t orv = 0;
+#pragma unroll
+    for (int i = 0; i < kValuesPerLane; ++i) orv |= v[i];
+    fast = full && orv < 8192u;
+    if (fast) {
+#pragma unroll
+      for (int i = 0; i < kValuesPerLane; ++i) my_bytes += 1u + (v[i] >= 64u);
+    }
+  }
+  // value i of the lane on the generic path
+  auto val = [&](int i) -> uint32_t {
+    if constexpr (sizeof(VT) == 2) return (pr[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+    else return v[i];
+  };
+  if (!fast) {
 #pragma unroll
     for (int i = 0; i < kValuesPerLane; ++i) {
-      const uint64_t z = (uint64_t)v[i] << 1;
+      const uint64_t z = (uint64_t)val(i) << 1;
       const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
       my_bytes += (e0 + i < L) ? len : 0u;
     }
@@ -142,19 +176,43 @@ __global__ void __launch_bounds__(kBlock)
   const uint32_t base = 32u + a - 64u * b0;  // LDS index of message byte `a`
   uint32_t pos = base + excl;
   if (fast) {
+    if constexpr (sizeof(VT) == 2) {
+      // Per pair: both 16-bit codes (byte 0 = low 7 bits of z = 2 v plus the
+      // continuation flag, byte 1 = z >> 7) by packed shifts and masks, then byte
+      // stores (unaligned 16-bit LDS stores work but measured at about half the
+      // rate of two byte stores). A one-byte value's second byte (zero) is
+      // overwritten by the next value of the lane (same lane, LDS program order);
+      // the lane's last value stores exactly its length.
 #pragma unroll
-    for (int i = 0; i < kValuesPerLane; ++i) {
-      const uint32_t z = v[i] << 1;
-      const uint32_t l2 = v[i] >= 64u;
-      lds[pos] = (uint8_t)((z & 0x7fu) | (l2 << 7));
-      if (i + 1 < kValuesPerLane || l2) lds[pos + 1] = (uint8_t)(z >> 7);
-      pos += 1u + l2;
+      for (int k = 0; k < kValuesPerLane / 2; ++k) {
+        const uint32_t p = pr[k];
+        const uint32_t f = ((p + 0x7fc07fc0u) >> 15) & 0x00010001u;  // value >= 64, per half
+        const uint32_t z2 = p << 1;
+        const uint32_t c2 = (z2 & 0x007f007fu) | ((z2 << 1) & 0x7f007f00u) | (f << 7);
+        lds[pos + 2 * k] = (uint8_t)c2;
+        lds[pos + 2 * k + 1] = (uint8_t)(c2 >> 8);
+        pos += f & 0xffffu;
+        lds[pos + 2 * k + 1] = (uint8_t)(c2 >> 16);
+        if (k + 1 < kValuesPerLane / 2 || (f >> 16)) lds[pos + 2 * k + 2] = (uint8_t)(c2 >> 24);
+        pos += f >> 16;
+      }
+    } else {
+      // each value stores both candidate bytes and the next value overwrites the
+      // second one when the varint was a single byte
+#pragma unroll
+      for (int i = 0; i < kValuesPerLane; ++i) {
+        const uint32_t z = v[i] << 1;
+        const uint32_t l2 = v[i] >= 64u;
+        lds[pos] = (uint8_t)((z & 0x7fu) | (l2 << 7));
+        if (i + 1 < kValuesPerLane || l2) lds[pos + 1] = (uint8_t)(z >> 7);
+        pos += 1u + l2;
+      }
     }
   } else {
 #pragma unroll
     for (int i = 0; i < kValuesPerLane; ++i) {
       if (e0 + i < L) {
-        const uint64_t z = (uint64_t)v[i] << 1;
+        const uint64_t z = (uint64_t)val(i) << 1;
         const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
 #pragma unroll
         for (int q = 0; q < 5; ++q)
