@@ -458,7 +458,10 @@ int main() {
       hc::os_random(reinterpret_cast<uint8_t*>(seedw), 8);
       uint32_t N = it < 60 ? seedw[0] % 400000u : seedw[0] % 70000u;
       if (it % 7 == 0) N &= ~15u;
-      if (it % 5 == 0) N = (N / kChunkBytes) * kChunkBytes + (uint32_t)(seedw[0] >> 24) - 40u + 40u * (N < 40u);
+      if (it % 5 == 0) {  // within -40 .. +215 bytes of a chunk border
+        const int64_t near = (int64_t)(N / kChunkBytes) * kChunkBytes + (int64_t)(seedw[0] >> 24) - 40;
+        N = (uint32_t)std::max<int64_t>(1, near);
+      }
       if (N == 0) N = 1;
       std::vector<uint8_t> ct(N + 16);
       if (it % 9 == 0) std::memset(ct.data(), 0xff, ct.size());
@@ -500,6 +503,33 @@ int main() {
     CHECK(accepted >= 10, "mod24 parameter search accepted only %d cases", accepted);
     CHECK(make_mod24(433, 7ull * 432 * 432).c != 0 && make_mod24(241, 5ull * 240 * 240).c != 0,
           "mod24 must cover the benchmark fields");
+  }
+  // 8. the encode kernel's packed varint pairs against a plain zigzag-LEB128 encoder:
+  //    every low value with a spread of high values, and the reverse
+  {
+    auto leb = [](uint32_t v, uint8_t (&out)[2]) {  // v < 2^13: one or two bytes
+      const uint32_t z = v << 1;
+      out[0] = (uint8_t)((z & 0x7f) | (z >= 128 ? 0x80 : 0));
+      out[1] = (uint8_t)(z >> 7);
+      return z >= 128 ? 2 : 1;
+    };
+    bool ok = true;
+    for (uint32_t a = 0; a < 8192 && ok; ++a) {
+      for (uint32_t b : {0u, 1u, 63u, 64u, 65u, 127u, 128u, 432u, 4095u, 8191u, (a * 2654435761u) >> 19}) {
+        for (int swap = 0; swap < 2 && ok; ++swap) {
+          const uint32_t lo = swap ? b : a, hi = swap ? a : b;
+          uint32_t codes, two;
+          varint_pair16(lo | (hi << 16), codes, two);
+          uint8_t el[2], eh[2];
+          const int nl = leb(lo, el), nh = leb(hi, eh);
+          ok = ok && (two & 0xffffu) == (uint32_t)(nl - 1) && (two >> 16) == (uint32_t)(nh - 1);
+          ok = ok && (codes & 0xffu) == el[0] && ((codes >> 8) & 0xffu) == el[1];
+          ok = ok && ((codes >> 16) & 0xffu) == eh[0] && (codes >> 24) == eh[1];
+          if (!ok) std::printf("  pair lo=%u hi=%u codes=%08x two=%08x\n", lo, hi, codes, two);
+        }
+      }
+    }
+    CHECK(ok, "varint_pair16 against zigzag LEB128");
   }
   std::printf(failures ? "host_emul: %d FAILURES\n" : "host_emul: all ok\n", failures);
   return failures ? 1 : 0;

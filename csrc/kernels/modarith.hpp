@@ -72,6 +72,16 @@ SDA_DEV uint32_t add_mod(uint32_t a, uint32_t b, uint32_t m) {
 SDA_DEV uint32_t sub_mod(uint32_t a, uint32_t b, uint32_t m) {
   return a >= b ? a - b : a + m - b;
 }
+// Zigzag-LEB128 codes of a pair of u16 values, both below 2^13 (codes of one or
+// two bytes; zigzag of a non-negative v is z = 2 v), computed on both halves of
+// the dword at once: half h of `codes` = byte 0 (low 7 bits of z, bit 7 = "a second
+// byte follows") | byte 1 (z >> 7) << 8, and bit 16 h of `two` = the value needs
+// two bytes (v >= 64). No step carries from the low half into the high one.
+SDA_DEV void varint_pair16(uint32_t p, uint32_t& codes, uint32_t& two) {
+  two = ((p + 0x7fc07fc0u) >> 15) & 0x00010001u;
+  const uint32_t z2 = p << 1;
+  codes = (z2 & 0x007f007fu) | ((z2 << 1) & 0x7f007f00u) | (two << 7);
+}
 // Canonical representative of a signed 32-bit input.
 SDA_DEV uint32_t canon_i32(int32_t s, const ModParams& P) {
   if (s >= 0 && (uint32_t)s < P.m) return (uint32_t)s;

@@ -18,6 +18,7 @@
 #include "block_utils.hpp"
 #include "device_crypto.hpp"
 #include "kernels.hpp"
+#include "modarith.hpp"
 
 namespace sdagpu {
 namespace {
@@ -185,10 +186,8 @@ __global__ void __launch_bounds__(kBlock)
       // the lane's last value stores exactly its length.
 #pragma unroll
       for (int k = 0; k < kValuesPerLane / 2; ++k) {
-        const uint32_t p = pr[k];
-        const uint32_t f = ((p + 0x7fc07fc0u) >> 15) & 0x00010001u;  // value >= 64, per half
-        const uint32_t z2 = p << 1;
-        const uint32_t c2 = (z2 & 0x007f007fu) | ((z2 << 1) & 0x7f007f00u) | (f << 7);
+        uint32_t c2, f;  // both 16-bit codes; bit 16 h: value h takes two bytes
+        varint_pair16(pr[k], c2, f);
         lds[pos + 2 * k] = (uint8_t)c2;
         lds[pos + 2 * k + 1] = (uint8_t)(c2 >> 8);
         pos += f & 0xffffu;
