@@ -274,8 +274,9 @@ def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
     T = G.sum_tiles(L)
     tile_sub = torch.empty(M, T + 1, dtype=torch.int32, device=dev)
     G.locate_tiles(pre, totals, L, tile_sub)
-    # participant groups: ~4k blocks fill the chip; u32 accumulators bound Pg
-    groups = max(1, min(P, -(-4096 // (T * rows))))
+    # participant groups: ~10k blocks, ten rounds of the 1024 that are resident at once (with
+    # ~4k the last, partly filled round cost 0.15 ms of 2.2); u32 accumulators bound Pg
+    groups = max(1, min(P, -(-10000 // (T * rows))))
     Pg = min(-(-P // groups), G.decode_sum_group_limit(m))
     part = torch.empty(-(-P // Pg), rows, L, dtype=torch.int32, device=dev)
     redo = torch.zeros(1, dtype=torch.int32, device=dev)
