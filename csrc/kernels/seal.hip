@@ -520,28 +520,18 @@ __global__ void __launch_bounds__(kBlock)
 constexpr int kMacChunksPerBlock = 8;  // k_mac_chunks: chunks of one message per block
 
 
-// Per-lane Horner Poly1305 partial of chunk k: lane t sums the 4 blocks ending
-// 4 (255 - t) blocks before the chunk end eb (end-aligned, so blocks before the
-// message start contribute zero) and scales by its factor r^(4 (255 - t)).
-// Handles what the matrix-core rows do not: a message's first chunk (its first
-// 32 bytes precede the message) and its last chunk (partial final block, short
-// tail). With all != 0 it runs every chunk (A/B measurement of the MFMA path).
-__global__ void __launch_bounds__(kBlock)
-    k_mac_horner(int K, const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
-                 const uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
-                 uint32_t* __restrict__ partials, int all) {
-  __shared__ uint64_t lsum[5][kWaves];
-  const int j = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t N = pt_len[j];
-  const int last = last_chunk(N);
-  int k;
-  if (all) {
-    k = blockIdx.x;
-    if (k > last) return;  // k_mac_chunks zeroes chunks past the message
-  } else {
-    k = blockIdx.x == 0 ? 0 : last;
-    if (blockIdx.x == 1 && last == 0) return;
-  }
+// Per-lane Horner Poly1305 partial of chunk k of message j, by the whole block:
+// lane t sums the 4 blocks ending 4 (255 - t) blocks before the chunk end eb
+// (end-aligned, so blocks before the message start contribute zero) and scales
+// by its factor r^(4 (255 - t)). Handles what the matrix-core rows do not: a
+// message's first chunk (its first 32 bytes precede the message) and its last
+// chunk (partial final block, short tail). Every ciphertext read of the chunk is
+// done when the function returns (the caller may then decrypt it in place).
+__device__ __forceinline__ void horner_chunk(int j, int k, int K, const MsgKey* __restrict__ keys,
+                                             const uint32_t* __restrict__ pows,
+                                             const uint8_t* __restrict__ ct, uint64_t stride, uint32_t N,
+                                             uint32_t* __restrict__ partials, uint64_t (*lsum)[kWaves]) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t kC = (int64_t)k * kChunkBytes;
   const int64_t start = kC >= 32 ? kC - 32 : 0;
   const int64_t end = min((int64_t)N, kC + kChunkBytes - 32);
@@ -593,6 +583,28 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
     for (int u = 0; u < 5; ++u) part[u] = (uint32_t)d[u];
   }
+  __syncthreads();  // lsum may be written again (the block's next edge chunk)
+}
+
+// The edge chunks alone (the encode kernel's own MAC covers the middle ones), or with
+// all != 0 every chunk (A/B measurement of the matrix-core path).
+__global__ void __launch_bounds__(kBlock)
+    k_mac_horner(int K, const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
+                 const uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
+                 uint32_t* __restrict__ partials, int all) {
+  __shared__ uint64_t lsum[5][kWaves];
+  const int j = blockIdx.y;
+  const uint32_t N = pt_len[j];
+  const int last = last_chunk(N);
+  int k;
+  if (all) {
+    k = blockIdx.x;
+    if (k > last) return;  // k_mac_chunks zeroes chunks past the message
+  } else {
+    k = blockIdx.x == 0 ? 0 : last;
+    if (blockIdx.x == 1 && last == 0) return;
+  }
+  horner_chunk(j, k, K, keys, pows, ct, stride, N, partials, lsum);
 }
 
 // out[q][u] = word 4 i + u of the 16-word block `w` held by lane q of this lane's
@@ -638,10 +650,14 @@ __device__ __forceinline__ void quad_transpose(uint32_t (&out)[4][4], const uint
 // int8 GEMM (device_crypto.hpp, poly_seg_value) with K = the row's 1 KiB of bytes
 // (wave w takes t in [16 w, 16 w + 16) of every row) and N = the 19 weight
 // digits (two 16-column tiles). Row i is then placed by r^(16 - i). First / last
-// chunks are k_mac_horner's (launched first: it reads the ciphertext this kernel
-// decrypts in place). With this K split wave w's operand bytes are exactly the
-// quarter [4096 w, 4096 (w + 1)) of the chunk.
-template <int DECRYPT>
+// chunks go through horner_chunk (by default in a k_mac_horner launch ahead of this
+// kernel: it reads the ciphertext this kernel decrypts in place). With this K split
+// wave w's operand bytes are exactly the quarter [4096 w, 4096 (w + 1)) of the chunk.
+// EDGES: the block also does its message's first / last chunk by Horner instead
+// of leaving them to a k_mac_horner launch (measured: the Horner code costs both
+// variants registers, 64 -> 92 and 112 -> 117 VGPRs, and the round 0.3 ms for the
+// 0.1 ms of launches it saves; selectable with set_mac_mfma(2), not the default).
+template <int DECRYPT, bool EDGES>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
     k_mac_chunks(int K, const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
                  uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
@@ -652,6 +668,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   // block, a lane per segment, instead of per chunk on one wave's 16 lanes
   __shared__ int32_t cacc[kMacChunksPerBlock][16][kPolyDigits + 1];
   __shared__ uint32_t scratch[kWaves];
+  __shared__ uint64_t lsum[EDGES ? 5 : 1][kWaves];
   const int j = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int row = lane & 15, g = lane >> 4;
@@ -702,6 +719,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     // serves the MAC and the decryption, and a wave reads only bytes it overwrites
     // itself, so the in-place decryption needs no barrier.
     const bool middle = use_mfma && k != 0 && k != last;
+    // EDGES: a message's first and last chunk by Horner here (block-uniform; its
+    // reads are done before the decryption below)
+    if constexpr (EDGES) {
+      if (use_mfma && !middle) horner_chunk(j, k, K, keys, pows, ct, stride, N, partials, lsum);
+    }
     uint4 d4[4];
     int64_t pos[4];
     bool in[4];
@@ -965,17 +987,17 @@ void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, u
                        uint64_t stride, const uint32_t* pt_len, uint32_t* partials, int decrypt,
                        uint32_t* term_cnt, uint32_t* sub_cnt, hipStream_t s) {
   if (M <= 0 || K <= 0) return;
-  // first / last chunks (every chunk when the matrix-core path is off) by
-  // Horner, ahead of the in-place decryption
-  hipLaunchKernelGGL(k_mac_horner, dim3(g_mac_mfma ? 2 : K, M), dim3(kBlock), 0, s, K, keys, pows,
-                     ct, stride, pt_len, partials, g_mac_mfma ? 0 : 1);
+  // first / last chunks (every chunk when the matrix-core path is off, mode 0) by
+  // Horner, ahead of the in-place decryption; mode 2 leaves them to k_mac_chunks
+  const bool edges = g_mac_mfma == 2;
+  if (!edges)
+    hipLaunchKernelGGL(k_mac_horner, dim3(g_mac_mfma ? 2 : K, M), dim3(kBlock), 0, s, K, keys, pows,
+                       ct, stride, pt_len, partials, g_mac_mfma ? 0 : 1);
   const dim3 grid_c((K + kMacChunksPerBlock - 1) / kMacChunksPerBlock, M);
-  if (decrypt)
-    hipLaunchKernelGGL(k_mac_chunks<1>, grid_c, dim3(kBlock), 0, s, K, keys, pows, ct, stride,
-                       pt_len, partials, term_cnt, sub_cnt, g_mac_mfma);
-  else
-    hipLaunchKernelGGL(k_mac_chunks<0>, grid_c, dim3(kBlock), 0, s, K, keys, pows, ct, stride,
-                       pt_len, partials, term_cnt, sub_cnt, g_mac_mfma);
+  auto kern = decrypt ? (edges ? k_mac_chunks<1, true> : k_mac_chunks<1, false>)
+                      : (edges ? k_mac_chunks<0, true> : k_mac_chunks<0, false>);
+  hipLaunchKernelGGL(kern, grid_c, dim3(kBlock), 0, s, K, keys, pows, ct, stride, pt_len, partials,
+                     term_cnt, sub_cnt, g_mac_mfma);
 }
 
 void launch_mac_final(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,

@@ -86,6 +86,35 @@ def test_host_seal_opens_on_gpu(cuda, native, L):
     assert out.cpu().tolist() == rows
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_mac_modes_seal_and_open(cuda, native, mode):
+    """The three Poly1305 arrangements give libsodium's tags on both sides: every
+    chunk by Horner (0), middle chunks on the matrix cores with the first / last
+    chunk in a launch of their own (1, the default), or inside the chunk kernel (2).
+    Lengths: one chunk, first + last only, and several middle chunks."""
+    from sda_amd._native import gpu
+    from sda_amd.ops.sealed import Arena, open_, seal
+    m = 433
+    keys = _keytable(native, cuda, 1)
+    gpu().set_mac_mfma(mode)
+    try:
+        for L in (5, 9000, 12000, 60000):
+            vals64 = torch.randint(0, m, (3, L), dtype=torch.int64)
+            kidx = torch.zeros(3, dtype=torch.int32, device=cuda)
+            err = torch.zeros(1, dtype=torch.int32, device=cuda)
+            arena = seal(vals64.to(torch.int16).to(cuda), kidx, keys.pks, os.urandom(32), 0, err, m)
+            blobs = arena.to_blobs()
+            for j in range(3):
+                pt = native.crypto.box_seal_open(blobs[j], keys.pk_bytes[0], keys.sk_bytes[0])
+                assert pt is not None and varint_decode(pt) == vals64[j].tolist(), (mode, L, j)
+            back = Arena.from_blobs(blobs, L, m, cuda)
+            out = open_(back, kidx, keys.sks, keys.pks, err, out_dtype=torch.int32)
+            assert int(err.item()) == 0, (mode, L)
+            assert torch.equal(out.cpu().to(torch.int64), vals64), (mode, L)
+    finally:
+        gpu().set_mac_mfma(1)
+
+
 def _open_sum_case(native, cuda, rows_, P, L, m, gen):
     """Host-sealed boxes (row-major: message r*P + p) -> open_sum vs a plain sum."""
     from sda_amd.ops.sealed import Arena, open_setup, open_sum
