@@ -141,8 +141,8 @@ PYBIND11_MODULE(_sda_gpu, m) {
                           P<const uint32_t>(pt_len), P<uint32_t>(partials), K, S(stream));
     check_launch("encode_encrypt");
   });
-  m.def("poly_powers", [](int M, uintptr_t keys, uintptr_t pows, uintptr_t stream) {
-    launch_poly_powers(M, P<const MsgKey>(keys), P<uint32_t>(pows), S(stream));
+  m.def("poly_powers", [](int M, uintptr_t keys, uintptr_t pows, int full, uintptr_t stream) {
+    launch_poly_powers(M, P<const MsgKey>(keys), P<uint32_t>(pows), full, S(stream));
     check_launch("poly_powers");
   });
   m.def("mac_edges", [](int M, int K, uintptr_t keys, uintptr_t pows, uintptr_t ct, uint64_t stride,

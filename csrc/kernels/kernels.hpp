@@ -147,7 +147,8 @@ void launch_mac_edges(int M, int K, const MsgKey* keys, const uint32_t* pows, co
 // varint-terminator counts per chunk).
 // Per-message Poly1305 tables pows [M][kPowWords]: chunk factors, segment
 // constant and weight digits of the matrix-core MAC (layout above).
-void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s);
+// full == 0: Horner factors only (enough for messages of at most two chunks)
+void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, int full, hipStream_t s);
 // With decrypt, term_cnt [M][K] (per chunk) and/or sub_cnt [M][K * kSubPerChunk]
 // (per 1 KiB sub-chunk) receive terminator counts (either may be null).
 void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,

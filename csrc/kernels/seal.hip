@@ -440,8 +440,11 @@ SDA_DEV P130 block_sum_p130(const P130& h, uint64_t (*red)[kWaves]) {
 //    row constant, the row factors r^(16 - i) and the pad-bit prefix sums
 //    (device_crypto.hpp, poly_seg_value / poly_row_const).
 // Depends only on the key: computed once per message on the side stream.
+// full == 0: only the Horner factors (messages of at most two chunks have no
+// middle chunk, so nothing reads the matrix-core tables: 5 KB instead of 26 KB per
+// message, which matters for the many-clerk sets' hundreds of thousands of boxes).
 __global__ void __launch_bounds__(kBlock)
-    k_poly_powers(const MsgKey* __restrict__ keys, uint32_t* __restrict__ pows, int prio) {
+    k_poly_powers(const MsgKey* __restrict__ keys, uint32_t* __restrict__ pows, int prio, int full) {
   if (prio) __builtin_amdgcn_s_setprio(3);  // side-stream key work (see k_seal_setup)
   __shared__ P130 rp[64];
   __shared__ uint64_t red[5][kWaves];
@@ -457,6 +460,7 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
     for (int u = 0; u < 5; ++u) base[t * 5 + u] = f.v[u];
   }
+  if (!full) return;  // block-uniform
   // R^(63 - t), R = r^16, for the blocks i + 16 t of a row
   P130 mine = p130_zero();
   if (t < 64) {
@@ -968,9 +972,9 @@ void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
 
 extern int g_powers_prio;  // keys.hip (set_key_prio)
 
-void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s) {
+void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, int full, hipStream_t s) {
   if (M <= 0) return;
-  hipLaunchKernelGGL(k_poly_powers, dim3(M), dim3(kBlock), 0, s, keys, pows, g_powers_prio);
+  hipLaunchKernelGGL(k_poly_powers, dim3(M), dim3(kBlock), 0, s, keys, pows, g_powers_prio, full);
 }
 
 void launch_mac_edges(int M, int K, const MsgKey* keys, const uint32_t* pows, const uint8_t* ct,

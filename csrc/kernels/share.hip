@@ -992,9 +992,31 @@ __global__ void __launch_bounds__(kBlock) k_count(int L, const VT* __restrict__ 
   const int e0 = t * kTileValues + threadIdx.x * 16;
   const VT* src = vals + (size_t)j * L;
   uint32_t bytes = 0;
+  if (e0 + 16 <= L) {
+    // 16-byte loads from an address that is only value-aligned (rows start at j * L)
+    struct __attribute__((packed, aligned(1))) Q { uint32_t w[4]; };
+    constexpr int kQ = (int)sizeof(VT) * 16 / 16;
+    const Q* q = reinterpret_cast<const Q*>(src + e0);
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (e0 + i < L) bytes += vlen((uint32_t)src[e0 + i]);
+    for (int i = 0; i < kQ; ++i) {
+      const Q d = q[i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if constexpr (sizeof(VT) == 4) {
+          bytes += vlen(d.w[u]);
+        } else if constexpr (sizeof(VT) == 2) {
+          bytes += vlen(d.w[u] & 0xffffu) + vlen(d.w[u] >> 16);
+        } else {
+          bytes += vlen(d.w[u] & 0xffu) + vlen((d.w[u] >> 8) & 0xffu) + vlen((d.w[u] >> 16) & 0xffu) +
+                   vlen(d.w[u] >> 24);
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (e0 + i < L) bytes += vlen((uint32_t)src[e0 + i]);
+  }
   uint32_t tot = block_sum(bytes, scratch);
   if (threadIdx.x == 0) cnt[(size_t)j * T + t] = tot;
 }

@@ -260,12 +260,14 @@ def encode_encrypt(vals, tile_off, keys, ct, stride, mac=None):
                           _ptr(ct), stride, pows, pt_len, partials, K, _stream())
 
 
-def poly_powers(M, keys, pows):
+def poly_powers(M, keys, pows, full=True):
     """Per-message Poly1305 tables (chunk factors for the Horner lanes; weight
-    digits, row factors and pad-bit prefixes for the matrix-core rows)."""
+    digits, row factors and pad-bit prefixes for the matrix-core rows). `full` =
+    False: the Horner factors only, which is all that messages of at most two
+    chunks (no middle chunk) ever read."""
     _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
     _check(pows, "pows", torch.int32, min_numel=M * POW_WORDS)
-    _gpu().poly_powers(M, _ptr(keys), _ptr(pows), _stream())
+    _gpu().poly_powers(M, _ptr(keys), _ptr(pows), 1 if full else 0, _stream())
 
 
 def mac_edges(M, K, keys, pows, ct, stride, pt_len, partials):

@@ -94,18 +94,33 @@ class KeySet:
     M: int
     keys: torch.Tensor  # uint8 [M * MSGKEY_BYTES]
     pows: torch.Tensor | None  # int32 [M * POW_WORDS]; None = not derived yet
+    K: int | None = None  # 16 KiB chunks per slot of the arena the keys were made for, if known
+    full: bool = True     # pows holds the matrix-core tables too (not only the Horner factors)
 
     @classmethod
-    def derive(cls, M: int, keys: torch.Tensor) -> "KeySet":
-        return cls(M, keys, None).with_powers()
+    def derive(cls, M: int, keys: torch.Tensor, K: int | None = None) -> "KeySet":
+        return cls(M, keys, None, K).with_powers()
 
     def with_powers(self) -> "KeySet":
-        """The Poly1305 tables (on the current stream) if not derived yet."""
+        """The Poly1305 tables (on the current stream) if not derived yet. Slots of at
+        most two chunks hold no middle chunk: only the Horner factors are made."""
         if self.pows is not None:
             return self
         pows = torch.empty(self.M * G.POW_WORDS, dtype=torch.int32, device=self.keys.device)
-        G.poly_powers(self.M, self.keys, pows)
-        return KeySet(self.M, self.keys, pows)
+        full = self.K is None or self.K > 2
+        G.poly_powers(self.M, self.keys, pows, full=full)
+        return KeySet(self.M, self.keys, pows, self.K, full)
+
+    def fit(self, arena: "Arena") -> "KeySet":
+        """The key set ready for `arena`'s messages: same message count, and the
+        complete tables if the arena's slots can hold a middle chunk (a set made for
+        short slots gets them now, on the current stream)."""
+        if self.M != arena.M:
+            raise ValueError("key set does not match the arena")
+        if self.pows is not None and not self.full and arena.K > 2:
+            G.poly_powers(self.M, self.keys, self.pows, full=True)
+            self.full = True
+        return self
 
     def slice(self, first: int, count: int) -> "KeySet":
         """Keys of messages [first, first+count) (no copy)."""
@@ -113,7 +128,8 @@ class KeySet:
             raise ValueError("key slice out of range")
         kb, pw = G.MSGKEY_BYTES, G.POW_WORDS
         return KeySet(count, self.keys[first * kb:(first + count) * kb],
-                      None if self.pows is None else self.pows[first * pw:(first + count) * pw])
+                      None if self.pows is None else self.pows[first * pw:(first + count) * pw],
+                      self.K, self.full)
 
     def record_stream(self, stream) -> None:
         self.keys.record_stream(stream)
@@ -143,7 +159,7 @@ def seal_setup(arena: Arena, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: 
     keys = torch.empty(arena.M * G.MSGKEY_BYTES, dtype=torch.uint8, device=arena.ct.device)
     G.seal_setup(arena.M, rng_key, owner_base, key_idx, pks, arena.ct, arena.stride, keys, err,
                  gate=gate)
-    return KeySet(arena.M, keys, None)
+    return KeySet(arena.M, keys, None, arena.K)
 
 
 def seal_encode(arena: Arena, keys: KeySet, values: torch.Tensor,
@@ -161,10 +177,8 @@ def seal_encode(arena: Arena, keys: KeySet, values: torch.Tensor,
         G.count(values, cnt)
     else:
         cnt = cnt.view(M, T)
-    if keys.M != M:
-        raise ValueError("key set does not match the arena")
     G.segscan(cnt, arena.pt_len)  # cnt becomes the tile byte offsets
-    keys = keys.with_powers()
+    keys = keys.with_powers().fit(arena)
     partials = None
     if FUSED_SEAL_MAC:
         # one pass: every tile adds its share of the middle chunks' Poly1305 partials
@@ -216,7 +230,7 @@ def open_setup(arena: Arena, key_idx: torch.Tensor, sks: torch.Tensor, pks: torc
     """X25519(sk, epk) + derivations for every slot (needs only the headers)."""
     keys = torch.empty(arena.M * G.MSGKEY_BYTES, dtype=torch.uint8, device=arena.ct.device)
     G.open_setup(arena.M, key_idx, sks, pks, arena.ct, arena.stride, keys, err, gate=gate)
-    return KeySet.derive(arena.M, keys)
+    return KeySet.derive(arena.M, keys, arena.K)
 
 
 def open_data(arena: Arena, keys: KeySet, err: torch.Tensor,
@@ -227,8 +241,7 @@ def open_data(arena: Arena, keys: KeySet, err: torch.Tensor,
     """
     M, L, K = arena.M, arena.L, arena.K
     dev = arena.ct.device
-    if keys.M != M:
-        raise ValueError("key set does not match the arena")
+    keys = keys.fit(arena)
     partials = torch.empty(M * K * 8, dtype=torch.int32, device=dev)
     term = torch.empty(M, K, dtype=torch.int32, device=dev)
     G.mac_chunks(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
@@ -258,8 +271,7 @@ def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
         raise ValueError("arena messages are not rows x participants")
     if m <= 0:
         raise ValueError("open_sum needs a modulus")
-    if keys.M != M:
-        raise ValueError("key set does not match the arena")
+    keys = keys.fit(arena)
     P = M // rows
     dev = arena.ct.device
     S = K * G.SUB_PER_CHUNK
