@@ -238,7 +238,14 @@ SDA_DEV uint32_t spread4(uint32_t bits4) {  // 4 bits -> 0xff per set bit, byte 
   return ((bits4 * 0x00204081u) & 0x01010101u) * 0xffu;
 }
 
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+//
+// kMaxBytes = 4 widens this to varints of up to four bytes (moduli up to 2^27, the
+// large packed-Shamir fields): a byte's shift is 7 x (length of the run of
+// continuation bytes right before it), a lane leaves the run of up to three
+// continuation bytes at its end to the next lane, which adds them from the four
+// bytes before its own; five-byte varints raise `redo`.
+template <int kMaxBytes>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMaxBytes > 2 ? 3 : 4)))
     k_decode_sum_z(int L, int P, int Pg, const uint8_t* __restrict__ pt, uint64_t stride,
                    const uint32_t* __restrict__ pt_len, int S, const uint32_t* __restrict__ pre,
                    const uint32_t* __restrict__ tile_sub, uint32_t* __restrict__ part,
@@ -335,7 +342,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
           if (hi > lo) {
             const uint64_t craw = ~term_mask64(w);
             if (lo > 0) K |= craw & (1ull << (lo - 1));
-            K &= ~(craw & (1ull << (hi - 1)));
+            uint64_t run = craw & (1ull << (hi - 1));  // continuation bytes at the end: the next lane's
+            if constexpr (kMaxBytes > 2) {
+              run |= (run >> 1) & craw;
+              run |= (run >> 1) & craw;
+            }
+            K &= ~run;
           }
           if (lo > 0 || hi <= lo) pm1 = 0;  // the byte before this lane is not its to add
 #pragma unroll
@@ -348,10 +360,19 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
           for (int q = 0; q < 16; ++q) tw[q] = ~w[q] & 0x80808080u;
           // a continuation byte in the last position belongs to the next lane's element
-          w[15] &= ~((uint32_t)((int32_t)w[15] >> 31) & 0xff000000u);
+          if constexpr (kMaxBytes <= 2) {
+            w[15] &= ~((uint32_t)((int32_t)w[15] >> 31) & 0xff000000u);
+          } else {  // ... the run of up to three of them
+            const uint32_t x15 = w[15];
+            const uint32_t t3 = (uint32_t)((int32_t)x15 >> 31);
+            const uint32_t t2 = t3 & (uint32_t)((int32_t)(x15 << 8) >> 31);
+            const uint32_t t1 = t2 & (uint32_t)((int32_t)(x15 << 16) >> 31);
+            w[15] = x15 & ~((t3 & 0xff000000u) | (t2 & 0x00ff0000u) | (t1 & 0x0000ff00u));
+          }
         }
         uint32_t c = 0;
-        {
+        uint32_t lead = 0;  // kMaxBytes > 2: what the continuation run before this lane adds
+        if constexpr (kMaxBytes <= 2) {
           uint32_t wp = pm1;
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
@@ -363,23 +384,51 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
           }
           bad |= (pm1 >> 24) & (pm1 >> 31) & 1u;                // ... of the byte before
           bad |= (pm1 >> 16) & (pm1 >> 24) & 0x80u;             // two continuation bytes before it
+        } else {
+          uint32_t wp = pm1;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const uint32_t x = w[q];
+            const uint32_t c1 = __builtin_amdgcn_alignbyte(x, wp, 3) & 0x80808080u;
+            const uint32_t c3 = c1 & __builtin_amdgcn_alignbyte(x, wp, 2) & __builtin_amdgcn_alignbyte(x, wp, 1);
+            bad |= x & c3;                                      // fourth continuation byte in a row
+            bad |= x & 0x01010101u & ~(c1 >> 7);                // odd first byte: a negative value
+            c += (uint32_t)__popc(tw[q]);
+            wp = x;
+          }
+          // the run of continuation bytes right before this lane (the previous lane left
+          // it out): b3 is the byte before, then b2, b1; its first byte has shift 0
+          const uint32_t b1 = (pm1 >> 8) & 0xffu, b2 = (pm1 >> 16) & 0xffu, b3 = pm1 >> 24;
+          const bool t3 = b3 & 0x80u, t2 = t3 && (b2 & 0x80u), t1 = t2 && (b1 & 0x80u);
+          lead = t1 ? ((b1 & 0x7fu) | ((b2 & 0x7fu) << 7) | ((b3 & 0x7fu) << 14))
+               : t2 ? ((b2 & 0x7fu) | ((b3 & 0x7fu) << 7))
+               : t3 ? (b3 & 0x7fu) : 0u;
+          bad |= lead & 1u;                                     // odd first byte of that run
+          bad |= pm1 & (pm1 >> 8) & (pm1 >> 16) & (pm1 >> 24) & 0x80u;  // four before it
         }
         const uint32_t incl = wave_incl_scan(c);
         const uint32_t total = wave_read_lane(incl, 63);
         // byte offset (within acc) of the rank of this lane's first terminator
         uint32_t a4 = 4u * (rank + kSumMargin - E0 + (incl - c));
-        lds_add(acc, a4, ((pm1 >> 24) & 0x7fu) & (0u - (pm1 >> 31)));
+        if constexpr (kMaxBytes <= 2) lds_add(acc, a4, ((pm1 >> 24) & 0x7fu) & (0u - (pm1 >> 31)));
+        else lds_add(acc, a4, lead);
         uint32_t wp = pm1;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const uint32_t x = w[q];
-          const uint32_t pc = (__builtin_amdgcn_alignbyte(x, wp, 3) & 0x80808080u) >> 7;
+          // continuation bytes right before each byte: 0 / 1, or the run length 0..3
+          uint32_t pc = (__builtin_amdgcn_alignbyte(x, wp, 3) & 0x80808080u) >> 7;
+          if constexpr (kMaxBytes > 2) {
+            const uint32_t c2 = pc & (__builtin_amdgcn_alignbyte(x, wp, 2) >> 7);
+            const uint32_t c3 = c2 & (__builtin_amdgcn_alignbyte(x, wp, 1) >> 7);
+            pc += c2 + c3;
+          }
           // (opaque steps: left to itself the compiler folds these shift-adds into
           // v_mul_lo_u32, a quarter-rate instruction, and the byte fields below
           // into bit-field extracts instead of free byte selects)
           uint32_t sh4 = pc << 3;
           asm volatile("" : "+v"(sh4));
-          sh4 -= pc;                            // 7 where the previous byte continues, per byte
+          sh4 -= pc;                            // 7 per continuation byte before, per byte
           uint32_t w7 = x & 0x7f7f7f7fu;
           // 4 * (terminators before byte u of this word), per byte
           uint32_t pre4 = tw[q] >> 5;           // 4 per terminator
@@ -532,10 +581,14 @@ void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* p
   dim3 grid(T, R, G);
   // lean kernel first where every canonical value is a 1- or 2-byte varint; the
   // generic one then runs only if `redo` was raised (it rewrites every slab)
-  const bool lean = g_decode_lean && redo != nullptr && m <= 8192u;
-  if (lean)
-    hipLaunchKernelGGL(k_decode_sum_z, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S, pre,
-                       tile_sub, part, redo, err);
+  // (codes of 2 bytes below 2^14, of 4 bytes below 2^28: moduli up to 2^13 / 2^27)
+  const bool lean = g_decode_lean && redo != nullptr && m <= (1u << 27);
+  if (lean && m <= 8192u)
+    hipLaunchKernelGGL(k_decode_sum_z<2>, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S,
+                       pre, tile_sub, part, redo, err);
+  else if (lean)
+    hipLaunchKernelGGL(k_decode_sum_z<4>, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S,
+                       pre, tile_sub, part, redo, err);
   const uint32_t* gate = lean ? redo : nullptr;
   if (m < 65536u)
     hipLaunchKernelGGL(k_decode_sum<true>, grid, dim3(kBlock), 0, s, L, P, Pg, mp, pt, stride,

@@ -341,8 +341,14 @@ def locate_tiles(pre: torch.Tensor, totals: torch.Tensor, L: int, tile_sub: torc
 
 def decode_sum_group_limit(modulus: int) -> int:
     """Most participants one decode-sum accumulator (u32) may add up: sums of
-    canonical values, or of 14-bit zigzag codes on the lean path (m <= 8192)."""
-    per = max(modulus - 1, 16383) if modulus <= 8192 else modulus - 1
+    canonical values, or on the lean path sums of zigzag codes of up to 14 bits
+    (m <= 2^13: two-byte varints) or 28 bits (m <= 2^27: four-byte varints)."""
+    if modulus <= 8192:
+        per = 16383
+    elif modulus <= 1 << 27:
+        per = (1 << 28) - 1
+    else:
+        per = modulus - 1
     return max(1, (2 ** 32 - 1) // max(1, per))
 
 
@@ -350,7 +356,7 @@ def decode_sum(rows: int, P: int, Pg: int, L: int, modulus: int, pt, stride, pt_
                tile_sub, part, out, err, redo=None):
     """out[r] = sum_p decode(message r*P + p) mod m (fused decode + combine).
 
-    `redo`: a zeroed int32 scratch word enabling the lean kernel (m <= 8192)."""
+    `redo`: a zeroed int32 scratch word enabling the lean kernels (m <= 2^27)."""
     M = rows * P
     S = pre.shape[1]
     if modulus <= 0:

@@ -156,11 +156,14 @@ def test_open_sum_matches_torch(cuda, native, L):
 
 @pytest.mark.parametrize("lean", [1, 0])
 @pytest.mark.parametrize("L,m", [(1, 433), (7, 433), (553, 433), (6144, 433), (6145, 433),
-                                 (20000, 433), (40000, 433), (30000, 8191), (9000, 64)])
+                                 (20000, 433), (40000, 433), (30000, 8191), (9000, 64),
+                                 (7, 5038849), (6145, 65521), (20000, 746497), (20000, 5038849),
+                                 (30000, (1 << 27) - 39)])
 def test_open_sum_canonical_streams(cuda, native, L, m, lean):
     """Canonical shares only (what our participants and any canonical encoder
-    produce): the lean kernel (sums of zigzag codes, k_decode_sum_z) and the
-    generic one (lean switched off) both equal the plain sum. Row kinds stress
+    produce): the lean kernels (sums of zigzag codes, k_decode_sum_z for varints of
+    up to two bytes, m <= 2^13, and of up to four, m <= 2^27) and the generic one
+    (lean switched off) both equal the plain sum. Row kinds stress
     the range edges: all-1-byte, all-2-byte, alternating and random streams
     drift apart by up to 2x in bytes, so 1 KiB sub-chunk cuts split varints."""
     from sda_amd._native import gpu
@@ -171,8 +174,9 @@ def test_open_sum_canonical_streams(cuda, native, L, m, lean):
             return [0] * L
         if kind == 1:
             return torch.randint(min(64, m - 1), m, (L,)).tolist()
-        if kind == 2:
-            return [(63 + (i & 1)) % m for i in range(L)]
+        if kind == 2:  # values on both sides of every varint length border
+            edge = [63, 64] if m <= 8192 else [63, 64, 8191, 8192, 1048575, 1048576]
+            return [edge[(i + i // 7) % len(edge)] % m for i in range(L)]
         if kind == 3:
             return [(m - 1) if (i % 3) else 1 for i in range(L)]
         return torch.randint(0, m, (L,)).tolist()
