@@ -120,6 +120,9 @@ __global__ void __launch_bounds__(kBlock)
   // Fast lanes (all 32 values present and < 2^13, i.e. 1- or 2-byte varints of
   // non-negative values) encode branch-free; other lanes take the generic path.
   bool fast;
+  // Middle lanes (all 32 values present and < 2^27: varints of up to four bytes, the
+  // large packed-Shamir fields) encode branch-free too, 32-bit arithmetic only.
+  bool mid = false;
   uint32_t my_bytes = 0;
   if constexpr (sizeof(VT) == 2) {
     // u16 pairs stay packed: both halves of a dword are handled by one
@@ -146,6 +149,7 @@ __global__ void __launch_bounds__(kBlock)
       for (int k = 0; k < kValuesPerLane / 2; ++k)
         my_bytes += (uint32_t)__popc((pr[k] + 0x7fc07fc0u) & 0x80008000u);
     }
+    mid = !fast && full;
   } else {
     load_values<VT>(v, src, e0, L);
     uint32_t orv = 0;
@@ -156,13 +160,20 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
       for (int i = 0; i < kValuesPerLane; ++i) my_bytes += 1u + (v[i] >= 64u);
     }
+    mid = !fast && full && orv < (1u << 27);
   }
-  // value i of the lane on the generic path
+  // value i of the lane on the generic paths
   auto val = [&](int i) -> uint32_t {
     if constexpr (sizeof(VT) == 2) return (pr[i >> 1] >> (16 * (i & 1))) & 0xffffu;
     else return v[i];
   };
-  if (!fast) {
+  if (mid) {
+#pragma unroll
+    for (int i = 0; i < kValuesPerLane; ++i) {
+      const uint32_t z = val(i) << 1;
+      my_bytes += 1u + (z >= (1u << 7)) + (z >= (1u << 14)) + (z >= (1u << 21));
+    }
+  } else if (!fast) {
 #pragma unroll
     for (int i = 0; i < kValuesPerLane; ++i) {
       const uint64_t z = (uint64_t)val(i) << 1;
@@ -206,6 +217,20 @@ __global__ void __launch_bounds__(kBlock)
         if (i + 1 < kValuesPerLane || l2) lds[pos + 1] = (uint8_t)(z >> 7);
         pos += 1u + l2;
       }
+    }
+  } else if (mid) {
+    // every value stores its four candidate bytes; what lies past its length is
+    // overwritten by the following values of the lane (each at least one byte), so
+    // byte k is stored unconditionally only where k more values follow
+#pragma unroll
+    for (int i = 0; i < kValuesPerLane; ++i) {
+      const uint32_t z = val(i) << 1;
+      const uint32_t l1 = z >= (1u << 7), l2 = z >= (1u << 14), l3 = z >= (1u << 21);
+      lds[pos] = (uint8_t)((z & 0x7fu) | (l1 << 7));
+      if (i + 1 < kValuesPerLane || l1) lds[pos + 1] = (uint8_t)(((z >> 7) & 0x7fu) | (l2 << 7));
+      if (i + 2 < kValuesPerLane || l2) lds[pos + 2] = (uint8_t)(((z >> 14) & 0x7fu) | (l3 << 7));
+      if (i + 3 < kValuesPerLane || l3) lds[pos + 3] = (uint8_t)(z >> 21);
+      pos += 1u + l1 + l2 + l3;
     }
   } else {
 #pragma unroll

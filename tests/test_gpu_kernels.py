@@ -39,7 +39,8 @@ def _keytable(native, cuda, count):
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("L,modulus", [(1, 433), (10, 433), (5000, 433), (20000, 433),
                                        (3000, 2 ** 31 - 1), (70000, 65521), (150001, 433),
-                                       (40000, 2 ** 31 - 1)])
+                                       (40000, 2 ** 31 - 1), (25000, 5038849), (7, 746497),
+                                       (8192, (1 << 27) - 39)])
 def test_gpu_seal_opens_on_host(cuda, native, monkeypatch, L, modulus, fused):
     """GPU-sealed boxes open on the host. `fused`: the tag's middle chunks computed
     inside the encode kernel (per tile, in LDS) instead of by a pass over the
