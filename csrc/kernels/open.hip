@@ -249,7 +249,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMa
     k_decode_sum_z(int L, int P, int Pg, const uint8_t* __restrict__ pt, uint64_t stride,
                    const uint32_t* __restrict__ pt_len, int S, const uint32_t* __restrict__ pre,
                    const uint32_t* __restrict__ tile_sub, uint32_t* __restrict__ part,
-                   uint32_t* redo, uint32_t* err) {
+                   uint32_t* redo, uint32_t* err, int three) {
+  // three (kMaxBytes = 4 only): the field's codes have at most three bytes, a fourth
+  // raises `redo` (the caller sized the participant groups for 21-bit codes)
   constexpr int kWaveBytes = 64 * 64;
   __shared__ uint32_t acc[kSumAcc];
   __shared__ uint32_t info[kBlock][4];
@@ -390,8 +392,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMa
           for (int q = 0; q < 16; ++q) {
             const uint32_t x = w[q];
             const uint32_t c1 = __builtin_amdgcn_alignbyte(x, wp, 3) & 0x80808080u;
-            const uint32_t c3 = c1 & __builtin_amdgcn_alignbyte(x, wp, 2) & __builtin_amdgcn_alignbyte(x, wp, 1);
-            bad |= x & c3;                                      // fourth continuation byte in a row
+            const uint32_t c2 = c1 & __builtin_amdgcn_alignbyte(x, wp, 2);
+            const uint32_t c3 = c2 & __builtin_amdgcn_alignbyte(x, wp, 1);
+            bad |= x & (three ? c2 : c3);                       // one continuation byte too many in a row
             bad |= x & 0x01010101u & ~(c1 >> 7);                // odd first byte: a negative value
             c += (uint32_t)__popc(tw[q]);
             wp = x;
@@ -404,7 +407,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMa
                : t2 ? ((b2 & 0x7fu) | ((b3 & 0x7fu) << 7))
                : t3 ? (b3 & 0x7fu) : 0u;
           bad |= lead & 1u;                                     // odd first byte of that run
-          bad |= pm1 & (pm1 >> 8) & (pm1 >> 16) & (pm1 >> 24) & 0x80u;  // four before it
+          // too many continuation bytes before it (a code of five / four bytes)
+          bad |= three ? (t1 ? 0x80u : 0u) : (pm1 & (pm1 >> 8) & (pm1 >> 16) & (pm1 >> 24) & 0x80u);
         }
         const uint32_t incl = wave_incl_scan(c);
         const uint32_t total = wave_read_lane(incl, 63);
@@ -585,10 +589,10 @@ void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* p
   const bool lean = g_decode_lean && redo != nullptr && m <= (1u << 27);
   if (lean && m <= 8192u)
     hipLaunchKernelGGL(k_decode_sum_z<2>, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S,
-                       pre, tile_sub, part, redo, err);
-  else if (lean)
+                       pre, tile_sub, part, redo, err, 0);
+  else if (lean)  // canonical codes 2 (m - 1) below 2^21 have at most three bytes
     hipLaunchKernelGGL(k_decode_sum_z<4>, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S,
-                       pre, tile_sub, part, redo, err);
+                       pre, tile_sub, part, redo, err, 2ull * (m - 1) < (1ull << 21) ? 1 : 0);
   const uint32_t* gate = lean ? redo : nullptr;
   if (m < 65536u)
     hipLaunchKernelGGL(k_decode_sum<true>, grid, dim3(kBlock), 0, s, L, P, Pg, mp, pt, stride,

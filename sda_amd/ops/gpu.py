@@ -342,11 +342,12 @@ def locate_tiles(pre: torch.Tensor, totals: torch.Tensor, L: int, tile_sub: torc
 def decode_sum_group_limit(modulus: int) -> int:
     """Most participants one decode-sum accumulator (u32) may add up: sums of
     canonical values, or on the lean path sums of zigzag codes of up to 14 bits
-    (m <= 2^13: two-byte varints) or 28 bits (m <= 2^27: four-byte varints)."""
+    (m <= 2^13: two-byte varints), 21 bits (2 (m - 1) < 2^21: three bytes) or 28 bits
+    (m <= 2^27: four bytes)."""
     if modulus <= 8192:
         per = 16383
-    elif modulus <= 1 << 27:
-        per = (1 << 28) - 1
+    elif modulus <= 1 << 27:  # a longer code than the field's raises the fallback
+        per = (1 << 21) - 1 if 2 * (modulus - 1) < 1 << 21 else (1 << 28) - 1
     else:
         per = modulus - 1
     return max(1, (2 ** 32 - 1) // max(1, per))

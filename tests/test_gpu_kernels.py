@@ -210,6 +210,19 @@ def test_open_sum_foreign_encodings(cuda, native):
     assert e == 0
     assert torch.equal(out, ref)
 
+    # mid-size fields (lean kernel for up to four bytes): a code one byte longer than
+    # the field's canonical ones, a negative value, a five-byte code -> generic decoder
+    for m, odd in ((65521, [2 ** 20 + 5]), (746497, [2 ** 20 + 5, -3]),
+                   (5038849, [2 ** 27 + 9]), (5038849, [-(2 ** 22)])):
+        def gen_mid(j, m=m, odd=odd):
+            row = torch.randint(0, m, (L,)).tolist()
+            for i in range(j + 1, L, 1013):
+                row[i] = odd[i % len(odd)]
+            return row
+        e, out, ref = _open_sum_case(native, cuda, 2, 5, L, m, gen_mid)
+        assert e == 0, (m, odd)
+        assert torch.equal(out, ref), (m, odd)
+
 
 def test_open_sum_flags_wrong_length(cuda, native):
     from sda_amd.ops.sealed import Arena, open_setup, open_sum
