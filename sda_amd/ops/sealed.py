@@ -287,8 +287,11 @@ def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
     tile_sub = torch.empty(M, T + 1, dtype=torch.int32, device=dev)
     G.locate_tiles(pre, totals, L, tile_sub)
     # participant groups: ~10k blocks, ten rounds of the 1024 that are resident at once (with
-    # ~4k the last, partly filled round cost 0.15 ms of 2.2); u32 accumulators bound Pg
-    groups = max(1, min(P, -(-10000 // (T * rows))))
+    # ~4k the last, partly filled round cost 0.15 ms of 2.2), but no fewer than 40
+    # participants per group (a block's fixed cost: clearing the LDS accumulator, writing
+    # its slab) unless that leaves fewer than ~4k blocks; u32 accumulators bound Pg
+    groups = max(-(-4096 // (T * rows)), min(-(-10000 // (T * rows)), P // 40))
+    groups = max(1, min(P, groups))
     Pg = min(-(-P // groups), G.decode_sum_group_limit(m))
     part = torch.empty(-(-P // Pg), rows, L, dtype=torch.int32, device=dev)
     redo = torch.zeros(1, dtype=torch.int32, device=dev)
