@@ -29,9 +29,10 @@ constexpr uint32_t kSigma0 = 0x61707865u, kSigma1 = 0x3320646eu, kSigma2 = 0x796
                    kSigma3 = 0x6b206574u;
 
 // ---------------------------------------------------------------- Salsa20 ---
+template <int kDoubleRounds = 10>
 SDA_DEV void salsa20_rounds(uint32_t (&x)[16]) {
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
+  for (int i = 0; i < kDoubleRounds; ++i) {
     x[4] ^= rotl32(x[0] + x[12], 7);   x[8] ^= rotl32(x[4] + x[0], 9);
     x[12] ^= rotl32(x[8] + x[4], 13);  x[0] ^= rotl32(x[12] + x[8], 18);
     x[9] ^= rotl32(x[5] + x[1], 7);    x[13] ^= rotl32(x[9] + x[5], 9);
@@ -60,6 +61,83 @@ SDA_DEV void salsa20_block(uint32_t (&out)[16], const uint32_t (&k)[8], uint32_t
 #pragma unroll
   for (int i = 0; i < 16; ++i) x[i] = j[i];
   salsa20_rounds(x);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) out[i] = x[i] + j[i];
+}
+
+// The part of a block's first double round that does not depend on the block counter
+// (its high word is zero: a message is far below 2^38 bytes): 60 of the 96 steps'
+// operations. Every lane of a wave works on one message, so these values are
+// wave-uniform: on the device the rotations are written for the scalar unit (which
+// has no rotate: two shifts and an or), so that the whole prefix runs there, beside
+// the vector work, instead of once per wave on the vector unit.
+template <int N>
+SDA_DEV uint32_t rotl32_uniform(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t hi, lo;
+  asm("s_lshl_b32 %0, %2, %3\n\ts_lshr_b32 %1, %2, %4"
+      : "=&s"(hi), "=&s"(lo)
+      : "s"(x), "n"(N), "n"(32 - N)
+      : "scc");
+  return hi | lo;
+#else
+  return rotl32(x, N);
+#endif
+}
+struct SalsaPrefix {
+  uint32_t x1, x2, x3, x9, x10, x13, x14, x15;  // after the column round
+  uint32_t x4c;                                 // x4 after the column round
+  uint32_t t8a;                                 // rotl(x4c + x0, 9): x8 after the column round = counter ^ t8a
+  uint32_t x4, x5, x6, x7;                      // after the row round (row 1 never sees the counter)
+  uint32_t x11;                                 // after its row step
+  uint32_t t8, t12;                             // what the row round xors into x8 and x12
+};
+SDA_DEV SalsaPrefix salsa20_prefix(const uint32_t (&k)[8], uint32_t n0, uint32_t n1) {
+  uint32_t x1 = k[0], x2 = k[1], x3 = k[2], x4 = k[3], x5 = kSigma1, x6 = n0, x7 = n1, x9 = 0,
+           x10 = kSigma2, x11 = k[4], x13 = k[6], x14 = k[7], x15 = kSigma3;
+  SalsaPrefix p;
+  x4 ^= rotl32_uniform<7>(kSigma0 + k[5]);
+  p.x4c = x4;
+  p.t8a = rotl32_uniform<9>(x4 + kSigma0);
+  x9 ^= rotl32_uniform<7>(x5 + x1);    x13 ^= rotl32_uniform<9>(x9 + x5);
+  x1 ^= rotl32_uniform<13>(x13 + x9);  x5 ^= rotl32_uniform<18>(x1 + x13);
+  x14 ^= rotl32_uniform<7>(x10 + x6);  x2 ^= rotl32_uniform<9>(x14 + x10);
+  x6 ^= rotl32_uniform<13>(x2 + x14);  x10 ^= rotl32_uniform<18>(x6 + x2);
+  x3 ^= rotl32_uniform<7>(x15 + x11);  x7 ^= rotl32_uniform<9>(x3 + x15);
+  x11 ^= rotl32_uniform<13>(x7 + x3);  x15 ^= rotl32_uniform<18>(x11 + x7);
+  p.x1 = x1; p.x2 = x2; p.x3 = x3; p.x9 = x9; p.x10 = x10; p.x13 = x13; p.x14 = x14; p.x15 = x15;
+  x6 ^= rotl32_uniform<7>(x5 + x4);    x7 ^= rotl32_uniform<9>(x6 + x5);
+  x4 ^= rotl32_uniform<13>(x7 + x6);   x5 ^= rotl32_uniform<18>(x4 + x7);
+  p.x4 = x4; p.x5 = x5; p.x6 = x6; p.x7 = x7;
+  x11 ^= rotl32_uniform<7>(x10 + x9);
+  p.x11 = x11;
+  p.t8 = rotl32_uniform<9>(x11 + x10);
+  p.t12 = rotl32_uniform<7>(x15 + x14);
+  return p;
+}
+// salsa20_block for a counter below 2^32, given the message's prefix.
+SDA_DEV void salsa20_block(uint32_t (&out)[16], const SalsaPrefix& p, const uint32_t (&k)[8],
+                           uint32_t n0, uint32_t n1, uint32_t ctr) {
+  uint32_t x[16];
+  x[8] = ctr ^ p.t8a;  // column 0: what is left of it
+  x[12] = k[5] ^ rotl32(x[8] + p.x4c, 13);
+  x[0] = kSigma0 ^ rotl32(x[12] + x[8], 18);
+  x[1] = p.x1 ^ rotl32(x[0] + p.x3, 7);  // row 0
+  x[2] = p.x2 ^ rotl32(x[1] + x[0], 9);
+  x[3] = p.x3 ^ rotl32(x[2] + x[1], 13);
+  x[0] ^= rotl32(x[3] + x[2], 18);
+  x[4] = p.x4; x[5] = p.x5; x[6] = p.x6; x[7] = p.x7;  // row 1
+  x[11] = p.x11;  // row 2
+  x[8] ^= p.t8;
+  x[9] = p.x9 ^ rotl32(x[8] + x[11], 13);
+  x[10] = p.x10 ^ rotl32(x[9] + x[8], 18);
+  x[12] ^= p.t12;  // row 3
+  x[13] = p.x13 ^ rotl32(x[12] + p.x15, 9);
+  x[14] = p.x14 ^ rotl32(x[13] + x[12], 13);
+  x[15] = p.x15 ^ rotl32(x[14] + x[13], 18);
+  salsa20_rounds<9>(x);
+  const uint32_t j[16] = {kSigma0, k[0], k[1], k[2], k[3], kSigma1, n0, n1,
+                          ctr, 0u, kSigma2, k[4], k[5], k[6], k[7], kSigma3};
 #pragma unroll
   for (int i = 0; i < 16; ++i) out[i] = x[i] + j[i];
 }

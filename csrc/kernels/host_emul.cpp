@@ -356,6 +356,15 @@ int main() {
     salsa20_block(sw, kw, n8w[0], n8w[1], 12345 + it);
     bytes(dsb, sw, 16);
     CHECK(std::memcmp(sb, dsb, 64) == 0, "salsa20");
+    {  // the same block from the message's counter-independent prefix
+      const SalsaPrefix pre = salsa20_prefix(kw, n8w[0], n8w[1]);
+      uint32_t pw[16];
+      salsa20_block(pw, pre, kw, n8w[0], n8w[1], (uint32_t)(12345 + it));
+      CHECK(std::memcmp(pw, sw, 64) == 0, "salsa20 from prefix");
+      salsa20_block(pw, pre, kw, n8w[0], n8w[1], 0xfffffff0u + (uint32_t)it);
+      salsa20_block(sw, kw, n8w[0], n8w[1], (uint64_t)(0xfffffff0u + (uint32_t)it));
+      CHECK(std::memcmp(pw, sw, 64) == 0, "salsa20 from prefix, large counter");
+    }
     uint8_t m64[64];
     hc::os_random(m64, 64);
     uint8_t b2[24], db2[24];

@@ -283,10 +283,12 @@ __global__ void __launch_bounds__(kBlock)
     }
   }
   const MsgKey key = keys[j];
+  // what the message's blocks have in common of their first double round (scalar unit)
+  const SalsaPrefix pre = salsa20_prefix(key.subkey, key.nonce[0], key.nonce[1]);
   const uint32_t nblk = (base + tile_bytes + 63) >> 6;
   for (uint32_t blk = tid; blk < nblk; blk += kBlock) {
     uint32_t w[16];
-    salsa20_block(w, key.subkey, key.nonce[0], key.nonce[1], (uint64_t)(b0 + blk));
+    salsa20_block(w, pre, key.subkey, key.nonce[0], key.nonce[1], b0 + blk);
     uint4* q = reinterpret_cast<uint4*>(lds + 64 * blk);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -725,6 +727,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     for (int i = tid; i < kMacChunksPerBlock * 16 * (kPolyDigits + 1); i += kBlock) flat[i] = 0;
     __syncthreads();
   }
+  // the message's key, and what its blocks have in common of their first double round
+  const MsgKey key = DECRYPT ? keys[j] : MsgKey{};
+  const SalsaPrefix pre = DECRYPT ? salsa20_prefix(key.subkey, key.nonce[0], key.nonce[1]) : SalsaPrefix{};
   for (int k = k0; k < k1; ++k) {
     const int64_t kC = (int64_t)k * kChunkBytes;
     const int64_t start = kC >= 32 ? kC - 32 : 0;
@@ -769,9 +774,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     // the four blocks their pieces lie in (piece q in block 16 q + j, words 4 i ..).
     uint32_t w[16];
     if constexpr (DECRYPT) {
-      const MsgKey key = keys[j];
-      const uint64_t blk = (uint64_t)(kC / 64) + 64 * wave + 16 * (lane & 3) + (lane >> 2);
-      salsa20_block(w, key.subkey, key.nonce[0], key.nonce[1], blk);
+      const uint32_t blk = (uint32_t)(kC / 64) + 64 * wave + 16 * (lane & 3) + (lane >> 2);
+      salsa20_block(w, pre, key.subkey, key.nonce[0], key.nonce[1], blk);
     }
     if (middle) {
       v4i acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
