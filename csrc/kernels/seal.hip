@@ -548,7 +548,7 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
-constexpr int kMacChunksPerBlock = 8;  // k_mac_chunks: chunks of one message per block
+constexpr int kMacChunksPerBlock = 8;  // k_mac_chunks: chunks of one message per block, at most
 
 
 // Per-lane Horner Poly1305 partial of chunk k of message j, by the whole block:
@@ -693,7 +693,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     k_mac_chunks(int K, const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
                  uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
                  uint32_t* __restrict__ partials, uint32_t* __restrict__ term_cnt,
-                 uint32_t* __restrict__ sub_cnt, int use_mfma) {
+                 uint32_t* __restrict__ sub_cnt, int use_mfma, int cpb) {
+  // cpb (<= kMacChunksPerBlock): chunks per block; fewer when the launch is small, so
+  // that the last, partly filled round of blocks costs less
   // digit sums of every (chunk of the block, segment): the four waves' K-slices
   // meet here through LDS adds, and the 130-bit work on them happens once per
   // block, a lane per segment, instead of per chunk on one wave's 16 lanes
@@ -707,8 +709,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   const int last = last_chunk(N);
   uint8_t* gmsg = ct + (size_t)j * stride + 48;
   const uint32_t* pw = pows + (size_t)j * kPowWords;
-  const int k0 = blockIdx.x * kMacChunksPerBlock;
-  const int k1 = min(K, k0 + kMacChunksPerBlock);
+  const int k0 = blockIdx.x * cpb;
+  const int k1 = min(K, k0 + cpb);
   const bool any_middle = use_mfma && k1 > 1 && k0 < last && max(k0, 1) < min(k1, last);
   // the message's weight-digit fragments (this lane's K-slice of its digit
   // columns): loaded once, reused by every chunk of the block
@@ -724,7 +726,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         b1[qq] = *reinterpret_cast<const v4i*>(tab + (16 + row) * kSegBytes + 64 * q + 16 * g);
     }
     int32_t* flat = &cacc[0][0][0];
-    for (int i = tid; i < kMacChunksPerBlock * 16 * (kPolyDigits + 1); i += kBlock) flat[i] = 0;
+    for (int i = tid; i < cpb * 16 * (kPolyDigits + 1); i += kBlock) flat[i] = 0;
     __syncthreads();
   }
   // the message's key, and what its blocks have in common of their first double round
@@ -845,7 +847,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   // digit sums into a 130-bit value and places it by r^(64 (15 - s)); the 16
   // lanes of a chunk then add up.
   __syncthreads();
-  if (tid < 16 * kMacChunksPerBlock) {
+  if (tid < 16 * cpb) {
     const int kk = tid >> 4, s = tid & 15, k = k0 + kk;
     const bool mid = k < k1 && k != 0 && k < last;
     P130 h = p130_zero();
@@ -1026,11 +1028,16 @@ void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, u
   if (!edges)
     hipLaunchKernelGGL(k_mac_horner, dim3(g_mac_mfma ? 2 : K, M), dim3(kBlock), 0, s, K, keys, pows,
                        ct, stride, pt_len, partials, g_mac_mfma ? 0 : 1);
-  const dim3 grid_c((K + kMacChunksPerBlock - 1) / kMacChunksPerBlock, M);
+  // 8 chunks per block amortise the weight fragments and the 130-bit tail; a launch of
+  // fewer than ~16 rounds of resident blocks (1024 - 2048 at a time) takes 4 per block
+  // (measured on the pipelined committee round: 4 waves -0.2 ms; 2 per block is worse)
+  int cpb = kMacChunksPerBlock;
+  while (cpb > 4 && (int64_t)M * ((K + cpb - 1) / cpb) < 16384) cpb /= 2;
+  const dim3 grid_c((K + cpb - 1) / cpb, M);
   auto kern = decrypt ? (edges ? k_mac_chunks<1, true> : k_mac_chunks<1, false>)
                       : (edges ? k_mac_chunks<0, true> : k_mac_chunks<0, false>);
   hipLaunchKernelGGL(kern, grid_c, dim3(kBlock), 0, s, K, keys, pows, ct, stride, pt_len, partials,
-                     term_cnt, sub_cnt, g_mac_mfma);
+                     term_cnt, sub_cnt, g_mac_mfma, cpb);
 }
 
 void launch_mac_final(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,
