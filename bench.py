@@ -206,11 +206,16 @@ def main():
     torch.cuda.synchronize()
     torch.cuda.reset_peak_memory_stats()
     res = None
+    host_s = 0.0  # host time spent queuing rounds (no synchronisation inside the loop)
+    if dist_mode:
+        comm.rendezvous_s = 0.0
     t0 = time.perf_counter()
     for i in range(args.steps):
         if i == args.corrupt_step:
             engine.corrupt_next_round()
+        th = time.perf_counter()
         res = agg.run_round(secrets, check=args.check)
+        host_s += time.perf_counter() - th
         err_total |= res.err  # device-side OR: read once, after the clock stops
         if args.check:
             verify(res, f"step {i}")
@@ -282,6 +287,11 @@ def main():
             "data": "synthetic uniform random participant vectors in [0, 433)",
             "hbm_high_water_bytes": hbm_peak,
             "xgmi": xgmi,
+            "host_ms_per_step": {"queuing_rounds": host_s / max(1, args.steps) * 1e3,
+                                 "of_which_store_rendezvous": (comm.rendezvous_s / max(1, args.steps) * 1e3
+                                                               if dist_mode else 0.0),
+                                 "note": "rank 0's host time inside run_round; the GPU runs behind "
+                                         "it, so it only bounds the step when it exceeds ms_per_step"},
             "pipeline_waves": waves if dist_mode else None,
             "pipeline_wave_tuning_ms": {str(k): v for k, v in wave_tuning.items()} or None,
             "timed_steps_verified": "device error word of every timed step (OR over steps and "

@@ -41,6 +41,7 @@ class Comm:
         self.device_native = self.backend == "nccl"
         self.deadline_s = float(deadline_s)
         self.audit: List[tuple] = []
+        self.rendezvous_s = 0.0  # host time spent in the store rendezvous (arrive / decide / decision)
         self._store = None
 
     # -- accounting -------------------------------------------------------------
@@ -185,7 +186,9 @@ class Comm:
 
     def arrive(self, topic: str, who) -> None:
         """Post "`who` reached `topic`" (non-blocking)."""
+        t0 = time.perf_counter()
         self.store.set(f"{topic}/at/{who}", b"1")
+        self.rendezvous_s += time.perf_counter() - t0
 
     def decide(self, topic: str, expected: Sequence, deadline_s: Optional[float] = None,
                all_or_nothing: bool = False, also: Sequence = ()) -> List:
@@ -194,6 +197,7 @@ class Comm:
         `also`, members the decider vouches for itself) for :meth:`decision`.
         With `all_or_nothing` an incomplete set is published as empty."""
         expected = list(expected)
+        t0 = time.perf_counter()
         deadline = time.monotonic() + (self.deadline_s if deadline_s is None else deadline_s)
         keys = {w: f"{topic}/at/{w}" for w in expected}
         live = expected
@@ -207,18 +211,22 @@ class Comm:
             live = []
         pub = [str(w) for w in live] + [str(w) for w in also]
         self.store.set(f"{topic}/live", ",".join(pub).encode() or b"-")
+        self.rendezvous_s += time.perf_counter() - t0
         return live
 
     def decision(self, topic: str, deadline_s: Optional[float] = None) -> List[str]:
         """The published outcome of :meth:`decide`. Blocks until it is there; a
         decider that never publishes (its process died) counts as "nobody"."""
         t = self.deadline_s if deadline_s is None else deadline_s
+        t0 = time.perf_counter()
         try:
             # the decider itself may wait a full deadline for stragglers first
             self.store.wait([f"{topic}/live"], timedelta(seconds=2 * t + 2))
+            v = self.store.get(f"{topic}/live").decode()
         except Exception:  # noqa: BLE001 - the store raises on timeout
             return []
-        v = self.store.get(f"{topic}/live").decode()
+        finally:
+            self.rendezvous_s += time.perf_counter() - t0
         return [] if v == "-" else v.split(",")
 
 
