@@ -71,8 +71,18 @@ SDA_DEV void load16_secrets(uint32_t (&x)[16], const int32_t* src, int valid, bo
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = i < valid ? src[i] : 0;
   }
+  // all 16 already canonical (the usual case): their OR is below m exactly then
+  // (a value is at most the OR; a negative one sets bit 31)
+  uint32_t any = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) x[i] = canon_i32(s[i], mp);
+  for (int i = 0; i < 16; ++i) any |= (uint32_t)s[i];
+  if (any < mp.m) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = (uint32_t)s[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = canon_i32(s[i], mp);
+  }
 }
 
 // rand-0.3 ChaChaRng block `ctr` (128-bit counter, here < 2^64) for a seed.
