@@ -286,6 +286,7 @@ def main():
             "dtype": "int32 (field elements mod 433; no floating point in this workload)",
             "data": "synthetic uniform random participant vectors in [0, 433)",
             "hbm_high_water_bytes": hbm_peak,
+            "hbm_reserved_bytes": torch.cuda.max_memory_reserved(),
             "xgmi": xgmi,
             "host_ms_per_step": {"queuing_rounds": host_s / max(1, args.steps) * 1e3,
                                  "of_which_store_rendezvous": (comm.rendezvous_s / max(1, args.steps) * 1e3

@@ -19,6 +19,7 @@ ChaCha20 streams (one per participant and purpose).
 """
 from __future__ import annotations
 
+import collections
 import os
 from dataclasses import dataclass, field
 from typing import Optional, Sequence
@@ -38,6 +39,8 @@ _TRACE = tracing_enabled()
 _OPEN_AFTER_SHARE = os.environ.get("SDA_OPEN_AFTER_SHARE", "1") == "1"
 # "open,powers" wave priorities of the side-stream key kernels (experiments)
 _KEY_PRIO = os.environ.get("SDA_KEY_PRIO")
+# unchecked rounds the host may queue ahead of the GPU (measurements of the unbounded case)
+_MAX_INFLIGHT = int(os.environ.get("SDA_MAX_INFLIGHT", "2"))
 
 
 class AggregationError(RuntimeError):
@@ -565,6 +568,19 @@ class DeviceAggregator:
 
     def _finish(self, err, marks, check, result: RoundResult) -> RoundResult:
         result.err = err
+        # At most two unchecked rounds in flight. The host queues a round in 1-2 ms, the
+        # GPU needs ~13: left alone the host runs dozens of rounds ahead, and every round
+        # in flight holds its own multi-GB arenas (a freed block that a second stream has
+        # touched is not reusable before the GPU has passed that use), so the allocator
+        # keeps mapping fresh memory instead of recycling.
+        inflight = getattr(self, "_inflight", None)
+        if inflight is None:
+            inflight = self._inflight = collections.deque()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        inflight.append(ev)
+        while len(inflight) > _MAX_INFLIGHT:
+            inflight.popleft().synchronize()
         if check or self.time_stages:
             e = int(err.item())
             if e:

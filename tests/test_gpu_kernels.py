@@ -304,6 +304,28 @@ def _round(cuda, spec, P, clerks=None):
     return res
 
 
+def test_unchecked_rounds_stay_two_deep(cuda):
+    """Unchecked rounds (no host read-back) may be queued at most two ahead of the GPU:
+    the host queues a round ten times faster than the GPU runs it, and every round in
+    flight holds its own arenas. Outputs of all of them stay correct."""
+    from sda_amd.engine import DeviceAggregator, reference_sum
+    from sda_amd.models import AggregationSpec, Additive
+    spec = AggregationSpec(20000, 433, Additive(3, 433))
+    agg = DeviceAggregator(spec, cuda)
+    secrets = torch.randint(0, 433, (16, 20000), dtype=torch.int32, device=cuda)
+    ref = reference_sum(secrets, 433)
+    outs = []
+    for _ in range(9):
+        res = agg.run_round(secrets, check=False)
+        outs.append((res.output, res.err))
+        assert len(agg._inflight) <= 2
+        assert all(ev.query() for ev in list(agg._inflight)[:-2]) or len(agg._inflight) <= 2
+    torch.cuda.synchronize()
+    for out, err in outs:
+        assert int(err.item()) == 0
+        assert torch.equal(out, ref)
+
+
 def test_round_additive(cuda):
     from sda_amd.models import AggregationSpec, Additive
     _round(cuda, AggregationSpec(10000, 433, Additive(3, 433)), 7)
