@@ -203,6 +203,7 @@ def gpu_configs(args):
               "share_storage": str(eng.vdtype).replace("torch.", ""),
               "layout": args.layout if world > 1 else "single GPU",
               "hbm_high_water_bytes": torch.cuda.max_memory_allocated(),
+              "hbm_reserved_bytes": torch.cuda.max_memory_reserved(),
               "wave": (args.wave or cfg.wave) if cfg.streamed else None, "correct": ok})
     if world > 1:
         dist.destroy_process_group()

@@ -566,13 +566,13 @@ class DeviceAggregator:
         of the dropped clerks' slots cost nothing more."""
         return [open_setup(arena, kidx, self.keys.sks, self.keys.pks, err)]
 
-    def _finish(self, err, marks, check, result: RoundResult) -> RoundResult:
-        result.err = err
-        # At most two unchecked rounds in flight. The host queues a round in 1-2 ms, the
-        # GPU needs ~13: left alone the host runs dozens of rounds ahead, and every round
-        # in flight holds its own multi-GB arenas (a freed block that a second stream has
-        # touched is not reusable before the GPU has passed that use), so the allocator
-        # keeps mapping fresh memory instead of recycling.
+    def throttle(self) -> None:
+        """Mark the end of a round (or streamed wave) on the current stream and wait
+        for the one before the previous: at most two in flight. The host queues a
+        round in 1-2 ms, the GPU needs ~13: left alone the host runs dozens of rounds
+        ahead, and every round in flight holds its own multi-GB arenas (a freed block
+        that a second stream has touched is not reusable before the GPU has passed
+        that use), so the allocator keeps mapping fresh memory instead of recycling."""
         inflight = getattr(self, "_inflight", None)
         if inflight is None:
             inflight = self._inflight = collections.deque()
@@ -581,6 +581,10 @@ class DeviceAggregator:
         inflight.append(ev)
         while len(inflight) > _MAX_INFLIGHT:
             inflight.popleft().synchronize()
+
+    def _finish(self, err, marks, check, result: RoundResult) -> RoundResult:
+        result.err = err
+        self.throttle()
         if check or self.time_stages:
             e = int(err.item())
             if e:

@@ -137,6 +137,7 @@ class StreamingAggregator:
                 if mask_acc is not None:
                     mask_acc += msum
             done += 1
+            eng.throttle()  # the host stays at most two waves ahead of the GPU
             last = w == waves - 1
             if self.checkpoint and ((w + 1) % self.every == 0 or last or
                                     (stop_after is not None and done >= stop_after)):
