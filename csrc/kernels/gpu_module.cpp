@@ -186,16 +186,20 @@ PYBIND11_MODULE(_sda_gpu, m) {
   });
   m.def("decode_sum", [](int R, int Pn, int Pg, int L, uint32_t mod, uintptr_t pt, uint64_t stride,
                          uintptr_t pt_len, int Sn, uintptr_t pre, uintptr_t tile_sub,
-                         uintptr_t part, uintptr_t out, uintptr_t err, uintptr_t redo,
+                         uintptr_t part, uintptr_t out, uintptr_t acc, uintptr_t err, uintptr_t redo,
                          uintptr_t stream) {
     if (mod == 0) throw std::invalid_argument("decode_sum: needs a modulus");
+    if (out == 0 && acc == 0) throw std::invalid_argument("decode_sum: needs out or acc");
     if ((uint64_t)Pg * (mod - 1) > 0xffffffffull)
       throw std::invalid_argument("decode_sum: Pg * (m - 1) overflows the u32 accumulators");
-    if (redo != 0 && mod <= 8192u && (uint64_t)Pg * 16383ull > 0xffffffffull)
-      throw std::invalid_argument("decode_sum: Pg * 16383 overflows the u32 accumulators");
+    // lean kernels add zigzag codes: up to 14 bits (two bytes), 21 (three) or 28 (four)
+    const uint64_t code_max = mod <= 8192u ? 16383ull
+                              : 2ull * (mod - 1) < (1ull << 21) ? (1ull << 21) - 1 : (1ull << 28) - 1;
+    if (redo != 0 && mod <= (1u << 27) && (uint64_t)Pg * code_max > 0xffffffffull)
+      throw std::invalid_argument("decode_sum: Pg codes overflow the u32 accumulators");
     launch_decode_sum(R, Pn, Pg, L, mod, P<const uint8_t>(pt), stride, P<const uint32_t>(pt_len), Sn,
                       P<const uint32_t>(pre), P<const uint32_t>(tile_sub), P<uint32_t>(part),
-                      P<uint32_t>(out), P<uint32_t>(err), P<uint32_t>(redo), S(stream));
+                      P<uint32_t>(out), P<int64_t>(acc), P<uint32_t>(err), P<uint32_t>(redo), S(stream));
     check_launch("decode_sum");
   });
   m.def("set_decode_lean", &set_decode_lean);

@@ -180,7 +180,8 @@ void launch_locate_tiles(int M, int S, int L, const uint32_t* pre, const uint32_
 // needs Pg * 16383 < 2^32 as well.
 void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* pt, uint64_t stride,
                        const uint32_t* pt_len, int S, const uint32_t* pre, const uint32_t* tile_sub,
-                       uint32_t* part, uint32_t* out, uint32_t* err, uint32_t* redo, hipStream_t s);
+                       uint32_t* part, uint32_t* out, int64_t* acc, uint32_t* err, uint32_t* redo,
+                       hipStream_t s);  // acc != null: acc[r][l] += the sums instead of writing out
 // Lean clerk decode (default on; 0 = generic kernel only) -- benchmarking switch.
 void set_decode_lean(int mode);
 // Column sums mod m: out[g][l] = sum_r vals[g][r][l] mod m.

@@ -461,12 +461,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMa
   if (malformed) atomicOr(err, kErrMalformed);
 }
 
-// out[x] = sum_g part[g][x] mod m   (x < X = rows * L)
+// out[x] = sum_g part[g][x] mod m   (x < X = rows * L); with `acc` the result is added
+// to acc[x] instead (the running sums of a round done in participant waves).
 // `zform` (may be null): *zform == 0 means the slabs hold sums of zigzag codes
 // (2 * value, from k_decode_sum_z) and are halved first.
 __global__ void __launch_bounds__(kBlock)
     k_sum_slabs(int G, int64_t X, ModParams mp, const uint32_t* __restrict__ part,
-                uint32_t* __restrict__ out, const uint32_t* zform) {
+                uint32_t* __restrict__ out, const uint32_t* zform, int64_t* __restrict__ acc) {
   const int64_t x = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
   if (x >= X) return;
   const int sh = (zform != nullptr && *zform == 0u) ? 1 : 0;
@@ -476,13 +477,20 @@ __global__ void __launch_bounds__(kBlock)
       const uint4 q = *reinterpret_cast<const uint4*>(part + g * X + x);
       a0 += q.x; a1 += q.y; a2 += q.z; a3 += q.w;
     }
-    *reinterpret_cast<uint4*>(out + x) = make_uint4(mod64(a0 >> sh, mp), mod64(a1 >> sh, mp),
-                                                     mod64(a2 >> sh, mp), mod64(a3 >> sh, mp));
+    const uint4 r = make_uint4(mod64(a0 >> sh, mp), mod64(a1 >> sh, mp), mod64(a2 >> sh, mp),
+                               mod64(a3 >> sh, mp));
+    if (acc != nullptr) {
+      acc[x] += r.x; acc[x + 1] += r.y; acc[x + 2] += r.z; acc[x + 3] += r.w;
+    } else {
+      *reinterpret_cast<uint4*>(out + x) = r;
+    }
   } else {
     for (int64_t y = x; y < min(X, x + 4); ++y) {
       uint64_t a = 0;
       for (int g = 0; g < G; ++g) a += part[g * X + y];
-      out[y] = mod64(a >> sh, mp);
+      const uint32_t r = mod64(a >> sh, mp);
+      if (acc != nullptr) acc[y] += r;
+      else out[y] = r;
     }
   }
 }
@@ -577,7 +585,8 @@ void launch_locate_tiles(int M, int S, int L, const uint32_t* pre, const uint32_
 
 void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* pt, uint64_t stride,
                        const uint32_t* pt_len, int S, const uint32_t* pre, const uint32_t* tile_sub,
-                       uint32_t* part, uint32_t* out, uint32_t* err, uint32_t* redo, hipStream_t s) {
+                       uint32_t* part, uint32_t* out, int64_t* acc, uint32_t* err, uint32_t* redo,
+                       hipStream_t s) {
   if (R <= 0 || P <= 0 || L <= 0 || Pg <= 0 || m == 0) return;
   const ModParams mp = make_mod_params(m);
   const int T = (L + kSumTile - 1) / kSumTile;
@@ -603,7 +612,7 @@ void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* p
   const int64_t X = (int64_t)R * L;
   const int64_t threads = (X + 3) / 4;
   hipLaunchKernelGGL(k_sum_slabs, dim3((unsigned)((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                     G, X, mp, part, out, gate);
+                     G, X, mp, part, out, gate, acc);
 }
 
 void launch_colsum(int G, int R, int L, uint32_t m, int value_bytes, const void* vals,

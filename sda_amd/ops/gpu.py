@@ -354,8 +354,9 @@ def decode_sum_group_limit(modulus: int) -> int:
 
 
 def decode_sum(rows: int, P: int, Pg: int, L: int, modulus: int, pt, stride, pt_len, pre,
-               tile_sub, part, out, err, redo=None):
-    """out[r] = sum_p decode(message r*P + p) mod m (fused decode + combine).
+               tile_sub, part, out, err, redo=None, acc=None):
+    """out[r] = sum_p decode(message r*P + p) mod m (fused decode + combine); with
+    `acc` (int64 [rows][L]) the sums are added to it instead and `out` may be None.
 
     `redo`: a zeroed int32 scratch word enabling the lean kernels (m <= 2^27)."""
     M = rows * P
@@ -372,10 +373,14 @@ def decode_sum(rows: int, P: int, Pg: int, L: int, modulus: int, pt, stride, pt_
     _check(pre, "pre", torch.int32, numel=M * S)
     _check(tile_sub, "tile_sub", torch.int32, numel=M * (sum_tiles(L) + 1))
     _check(part, "part", torch.int32, numel=groups * rows * L)
-    _check(out, "out", torch.int32, numel=rows * L)
+    if acc is not None:
+        _check(acc, "acc", torch.int64, numel=rows * L)
+    else:
+        _check(out, "out", torch.int32, numel=rows * L)
     _check(err, "err", torch.int32, numel=1)
     _gpu().decode_sum(rows, P, Pg, L, modulus, _ptr(pt), stride, _ptr(pt_len), S, _ptr(pre),
-                      _ptr(tile_sub), _ptr(part), _ptr(out), _ptr(err),
+                      _ptr(tile_sub), _ptr(part), _ptr(out) if acc is None else 0,
+                      _ptr(acc) if acc is not None else 0, _ptr(err),
                       _ptr(redo) if redo is not None else 0, _stream())
 
 

@@ -256,9 +256,10 @@ def open_data(arena: Arena, keys: KeySet, err: torch.Tensor,
 
 
 def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
-             out: torch.Tensor) -> torch.Tensor:
+             out: torch.Tensor | None, acc: torch.Tensor | None = None) -> torch.Tensor:
     """Verify + decrypt + decode + combine: out[r] = sum over p of the values of
-    message r * P + p, mod the arena modulus (P = M / rows).
+    message r * P + p, mod the arena modulus (P = M / rows). With `acc` (int64
+    [rows][L], contiguous) the sums are added to it instead (rounds done in waves).
 
     The clerk's open-and-combine (reference clerk.rs:79-86) without
     materialising decoded shares: the MAC pass counts varint terminators per
@@ -296,8 +297,8 @@ def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
     part = torch.empty(-(-P // Pg), rows, L, dtype=torch.int32, device=dev)
     redo = torch.zeros(1, dtype=torch.int32, device=dev)
     G.decode_sum(rows, P, Pg, L, m, arena.ct, arena.stride, arena.pt_len, pre, tile_sub, part,
-                 out, err, redo)
-    return out
+                 out, err, redo, acc=acc)
+    return out if acc is None else acc
 
 
 def open_(arena: Arena, key_idx: torch.Tensor, sks: torch.Tensor, pks: torch.Tensor,

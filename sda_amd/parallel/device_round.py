@@ -286,22 +286,22 @@ class DeviceCommittee:
                 # equal segments side by side: one launch, a row per clerk
                 first, _ = pl.segment_rows(segs[0][0])
                 rows = len(segs) * W * segs[0][1].count
-                out = torch.empty(len(segs), B, dtype=torch.int32, device=dev)
-                open_sum(inbox.slice(base + first, rows), ko.slice(base + first, rows), err,
-                         rows=len(segs), out=out)
-                c0 = segs[0][1].clerk  # side-by-side segments are consecutive clerks
+                c0 = segs[0][1].clerk  # side-by-side segments are mostly consecutive clerks
                 if [s.clerk for _, s in segs] == list(range(c0, c0 + len(segs))):
-                    acc[c0:c0 + len(segs)] += out
+                    # the sums go straight into the clerks' running rows
+                    open_sum(inbox.slice(base + first, rows), ko.slice(base + first, rows), err,
+                             rows=len(segs), out=None, acc=acc[c0:c0 + len(segs)])
                 else:
+                    out = torch.empty(len(segs), B, dtype=torch.int32, device=dev)
+                    open_sum(inbox.slice(base + first, rows), ko.slice(base + first, rows), err,
+                             rows=len(segs), out=out)
                     for j, (_, s) in enumerate(segs):
                         acc[s.clerk] += out[j]
             else:
                 for i, s in segs:
                     first, rows = pl.segment_rows(i)
-                    out = torch.empty(B, dtype=torch.int32, device=dev)
                     open_sum(inbox.slice(base + first, rows), ko.slice(base + first, rows), err,
-                             rows=1, out=out)
-                    acc[s.clerk] += out
+                             rows=1, out=None, acc=acc[s.clerk])
 
         pending = None
         G.gate_wait(gate)
