@@ -471,18 +471,33 @@ __global__ void __launch_bounds__(kBlock)
   const int64_t x = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
   if (x >= X) return;
   const int sh = (zform != nullptr && *zform == 0u) ? 1 : 0;
-  if (x + 4 <= X && (X % 4) == 0) {
+  if (x + 4 <= X) {
+    // 16-byte loads at 4-byte alignment: slab g starts at g * X words, X any length
+    // (333,334 batches in the packed-Shamir rounds)
+    struct __attribute__((packed, aligned(4))) Q {
+      uint32_t w[4];
+    };
     uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    for (int g = 0; g < G; ++g) {
-      const uint4 q = *reinterpret_cast<const uint4*>(part + g * X + x);
-      a0 += q.x; a1 += q.y; a2 += q.z; a3 += q.w;
+    int g = 0;
+    for (; g + 8 <= G; g += 8) {  // eight slabs' loads in flight at once (the slabs are far apart)
+      Q q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] = *reinterpret_cast<const Q*>(part + (int64_t)(g + u) * X + x);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a0 += q[u].w[0]; a1 += q[u].w[1]; a2 += q[u].w[2]; a3 += q[u].w[3];
+      }
+    }
+    for (; g < G; ++g) {
+      const Q q = *reinterpret_cast<const Q*>(part + (int64_t)g * X + x);
+      a0 += q.w[0]; a1 += q.w[1]; a2 += q.w[2]; a3 += q.w[3];
     }
     const uint4 r = make_uint4(mod64(a0 >> sh, mp), mod64(a1 >> sh, mp), mod64(a2 >> sh, mp),
                                mod64(a3 >> sh, mp));
     if (acc != nullptr) {
       acc[x] += r.x; acc[x + 1] += r.y; acc[x + 2] += r.z; acc[x + 3] += r.w;
     } else {
-      *reinterpret_cast<uint4*>(out + x) = r;
+      *reinterpret_cast<Q*>(out + x) = Q{{r.x, r.y, r.z, r.w}};  // `out` may be a row of a wider tensor
     }
   } else {
     for (int64_t y = x; y < min(X, x + 4); ++y) {
