@@ -255,6 +255,20 @@ def open_data(arena: Arena, keys: KeySet, err: torch.Tensor,
     return out
 
 
+def decode_group_size(P: int, tiles_x_rows: int, limit: int) -> int:
+    """Participants per decode-sum block (a block sums one element tile of one row
+    over a group of participants; the groups' slabs are added afterwards).
+
+    Aim: ~10k blocks -- ten rounds of the 1024 that are resident at once (with ~4k
+    the last, partly filled round cost 0.15 ms of 2.2) -- but no fewer than 40
+    participants per group (a block's fixed cost: clearing the LDS accumulator,
+    writing its slab) unless that leaves fewer than ~4k blocks. `limit`: what the
+    u32 accumulators can add up (:func:`gpu.decode_sum_group_limit`)."""
+    groups = max(-(-4096 // tiles_x_rows), min(-(-10000 // tiles_x_rows), P // 40))
+    groups = max(1, min(P, groups))
+    return max(1, min(-(-P // groups), limit))
+
+
 def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
              out: torch.Tensor | None, acc: torch.Tensor | None = None) -> torch.Tensor:
     """Verify + decrypt + decode + combine: out[r] = sum over p of the values of
@@ -287,13 +301,7 @@ def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
     T = G.sum_tiles(L)
     tile_sub = torch.empty(M, T + 1, dtype=torch.int32, device=dev)
     G.locate_tiles(pre, totals, L, tile_sub)
-    # participant groups: ~10k blocks, ten rounds of the 1024 that are resident at once (with
-    # ~4k the last, partly filled round cost 0.15 ms of 2.2), but no fewer than 40
-    # participants per group (a block's fixed cost: clearing the LDS accumulator, writing
-    # its slab) unless that leaves fewer than ~4k blocks; u32 accumulators bound Pg
-    groups = max(-(-4096 // (T * rows)), min(-(-10000 // (T * rows)), P // 40))
-    groups = max(1, min(P, groups))
-    Pg = min(-(-P // groups), G.decode_sum_group_limit(m))
+    Pg = decode_group_size(P, T * rows, G.decode_sum_group_limit(m))
     part = torch.empty(-(-P // Pg), rows, L, dtype=torch.int32, device=dev)
     redo = torch.zeros(1, dtype=torch.int32, device=dev)
     G.decode_sum(rows, P, Pg, L, m, arena.ct, arena.stride, arena.pt_len, pre, tile_sub, part,

@@ -126,3 +126,28 @@ def test_wave_bounds_cover_the_participants(waves, P):
     if waves == "taper" and P >= 16:
         sizes = [hi - lo for lo, hi in bounds]
         assert sizes[0] <= sizes[2] and sizes[-1] <= sizes[-3]
+
+
+def test_decode_group_size_rule():
+    """Participant groups of the clerk's decode + sum: the u32 accumulators' limit is
+    never exceeded, groups cover all participants, the headline shape gets ~10k blocks,
+    per-clerk opens keep at least 40 participants per block, and small waves still get
+    ~4k blocks."""
+    from sda_amd.ops.gpu import decode_sum_group_limit
+    from sda_amd.ops.sealed import decode_group_size
+    for P in (1, 2, 7, 39, 40, 125, 250, 1000, 10000):
+        for tr in (1, 2, 163, 489, 815, 1304, 20346 * 8):
+            for m in (2, 433, 8191, 65521, 746497, 5038849, (1 << 27) - 39, 2 ** 31 - 1):
+                lim = decode_sum_group_limit(m)
+                pg = decode_group_size(P, tr, lim)
+                assert 1 <= pg <= min(P, lim) or (pg == 1 and P >= 1)
+                groups = -(-P // pg)
+                assert groups * pg >= P
+    lim = decode_sum_group_limit(433)
+    assert 9000 <= -(-1000 // decode_group_size(1000, 489, lim)) * 489 <= 11000   # headline
+    assert decode_group_size(1000, 163, lim) >= 38                                  # one clerk's row
+    assert -(-125 // decode_group_size(125, 489, lim)) * 489 >= 4096                # an 8-wave slice
+    # code lengths decide the limit on the lean path
+    assert decode_sum_group_limit(433) == (2 ** 32 - 1) // 16383
+    assert decode_sum_group_limit(746497) == (2 ** 32 - 1) // (2 ** 21 - 1)
+    assert decode_sum_group_limit(5038849) == (2 ** 32 - 1) // (2 ** 28 - 1)
