@@ -638,42 +638,6 @@ __global__ void __launch_bounds__(kBlock)
   horner_chunk(j, k, K, keys, pows, ct, stride, N, partials, lsum);
 }
 
-// out[q][u] = word 4 i + u of the 16-word block `w` held by lane q of this lane's
-// quad, i = this lane's position in the quad: a 4 x 4 transpose of 4-word groups
-// over the quad's lanes in two butterfly steps (lane ^ 1, then lane ^ 2), moved by
-// DPP quad permutes. After step 1 slot s holds group (s & 2) | (i & 1) of lane
-// (i & 2) | (s & 1); step 2 exchanges slot pairs with lane ^ 2.
-template <int CTRL>
-__device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xf, 0xf, true);
-}
-__device__ __forceinline__ void quad_transpose(uint32_t (&out)[4][4], const uint32_t (&w)[16], int lane) {
-  constexpr int kSwap1 = 0xB1;  // quad_perm [1, 0, 3, 2]
-  constexpr int kSwap2 = 0x4E;  // quad_perm [2, 3, 0, 1]
-  const bool odd = lane & 1, hi = lane & 2;
-  uint32_t a[4][4];
-#pragma unroll
-  for (int gp = 0; gp < 4; gp += 2) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t g0 = w[4 * gp + u], g1 = w[4 * (gp + 1) + u];
-      const uint32_t p0 = quad_perm<kSwap1>(g0), p1 = quad_perm<kSwap1>(g1);  // the partner's
-      a[gp][u] = odd ? p1 : g0;
-      a[gp + 1][u] = odd ? g1 : p0;
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t lo_ = a[s][u], hi_ = a[s + 2][u];
-      const uint32_t plo = quad_perm<kSwap2>(lo_), phi = quad_perm<kSwap2>(hi_);
-      out[s][u] = hi ? phi : lo_;
-      out[s + 2][u] = hi ? hi_ : plo;
-    }
-  }
-}
-
 // Middle chunks on the matrix cores (+ in-place decryption and terminator
 // counts for every chunk when DECRYPT). A middle chunk (not the message's
 // first or last) is 1024 full blocks starting at block fb = kC/16 - 2, taken as
@@ -702,6 +666,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   __shared__ int32_t cacc[kMacChunksPerBlock][16][kPolyDigits + 1];
   __shared__ uint32_t scratch[kWaves];
   __shared__ uint64_t lsum[EDGES ? 5 : 1][kWaves];
+  __shared__ __attribute__((aligned(16))) uint32_t kst[DECRYPT ? kWaves * 1024 : 4];  // keystream, per wave
   const int j = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int row = lane & 15, g = lane >> 4;
@@ -797,11 +762,28 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     }
 
     if constexpr (DECRYPT) {
-      // 4 x 4 transpose of the keystream's word groups within each quad (two
-      // butterfly steps on the VALU): afterwards ks[q] = words 4 i .. 4 i + 3 of the
-      // block of quad lane q, i.e. the keystream of piece q
+      // The keystream to the pieces' layout (ks[q] = words 4 i .. 4 i + 3 of the block
+      // that quad lane q computed, i = this lane's place in its quad) through the
+      // wave's own 4 KiB of LDS: four 16-byte stores and loads instead of a 64-
+      // instruction butterfly on the VALU, which is what bounds this kernel while
+      // its LDS port idles. Block b lies at word 16 b; the lane that computed it
+      // (place i) rotates its four word groups by i slots, so that 8 consecutive
+      // lanes of a store or a load cover all 32 banks. Same wave, LDS keeps program
+      // order: no barrier.
       uint32_t ks[4][4];
-      quad_transpose(ks, w, lane);
+      {
+        uint32_t* kw = kst + 1024 * wave;
+        const int i4 = lane & 3, j4 = lane >> 2;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          *reinterpret_cast<uint4*>(kw + 16 * (16 * i4 + j4) + 4 * ((u + i4) & 3)) =
+              make_uint4(w[4 * u], w[4 * u + 1], w[4 * u + 2], w[4 * u + 3]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint4 t = *reinterpret_cast<const uint4*>(kw + 16 * (16 * q + j4) + 4 * ((i4 + q) & 3));
+          ks[q][0] = t.x; ks[q][1] = t.y; ks[q][2] = t.z; ks[q][3] = t.w;
+        }
+      }
       uint32_t cnt[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
