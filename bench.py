@@ -24,8 +24,14 @@ non-private upper bound (each GPU opens its own participants' boxes and the
 plaintext partial sums are reduced): it shows what the all-to-all costs.
 
 Launch: python bench.py --gpus 1 --steps 5 --warmup 2
+        python bench.py --gpus N --steps K --warmup W      (starts its own N ranks)
         python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
             --master-port P bench.py --gpus N --steps K --warmup W
+
+`--gpus N` with N > 1 and no rendezvous environment starts the N ranks itself: the
+parent process runs `python -m torch.distributed.run` as a child before it has
+imported torch or touched a GPU, relays rank 0's JSON line and exits with the
+launcher's return code.
 """
 from __future__ import annotations
 
@@ -102,30 +108,119 @@ def parse():
                     help="run the distributed engine even on one rank (measures its overhead)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU")
+    ap.add_argument("--engine", default="device", choices=["device", "host"],
+                    help="device = the HIP kernels on cuda:LOCAL_RANK. host = the C++ client "
+                         "engines on the CPU over gloo: a rehearsal of the launch, exchange and "
+                         "result paths on a machine without GPUs (use small --participants / "
+                         "--dim); its numbers are not the benchmark")
     ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="process-group timeout in seconds: a rank that loses a peer exits non-zero")
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="override GPU_MAX_HW_QUEUES for this process (A/B measurements); 0 = leave "
                          "the environment's value, which is also what measured fastest")
+    ap.add_argument("--loopback", action="store_true",
+                    help="with --force-dist on one rank: the rank's own piece of every exchange "
+                         "(ephemeral-key headers, sealed boxes, result boxes) goes through an RCCL "
+                         "send/recv to itself instead of a local copy, so the point-to-point path "
+                         "and its stream ordering run on a one-GPU machine")
     ap.add_argument("--corrupt-step", type=int, default=-1,
                     help="fault injection: flip a ciphertext bit in this timed step (the run must fail)")
     return ap.parse_args()
 
 
+def launcher_env(args):
+    """(world, rank, local_rank) from the launcher's environment; a plain command
+    line that wants the distributed engine on one rank gets a rendezvous of its own."""
+    if (args.force_dist or args.engine == "host") and "MASTER_ADDR" not in os.environ:
+        from sda_amd.utils.launch import free_port
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0",
+                          WORLD_SIZE="1", LOCAL_RANK="0")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)",
+              file=sys.stderr)
+        sys.exit(2)
+    return world, rank, local_rank
+
+
+def host_rehearsal(args):
+    """The N-rank committee round on the CPU engines over gloo: same launcher,
+    same plan, same exchange / partial / result stages as the device run, with
+    the reference's per-participant client code in place of the kernels."""
+    import numpy as np
+    import torch.distributed as dist
+
+    from sda_amd.models.schemes import Additive, AggregationSpec, NoMask
+    from sda_amd.parallel.engine import DistributedAggregator
+
+    world, rank, _ = launcher_env(args)
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.dist_timeout))
+    spec = AggregationSpec(args.dim, args.modulus, Additive(args.clerks, args.modulus), NoMask(),
+                           title="bench")
+    P, m = args.participants, args.modulus
+    agg = DistributedAggregator(spec, engine="host", layout=args.layout,
+                                deadline_s=min(60.0, args.dist_timeout / 4),
+                                loopback=args.loopback)
+    comm = agg.comm
+    secrets = np.random.default_rng(1234 + rank).integers(0, m, size=(P, args.dim), dtype=np.int64)
+    total = comm.reduce_sum(secrets.sum(0), dst=0)
+    expected = np.remainder(total, m) if rank == 0 else None
+
+    def verify(res, what):
+        if rank == 0 and not np.array_equal(res.output, expected):
+            raise SystemExit(f"bench: {what}: aggregate does not match the reference sum")
+
+    for i in range(args.warmup):
+        verify(agg.run_round(secrets), f"warmup round {i}")
+    comm.reset_audit()
+    comm.barrier()
+    t0 = time.perf_counter()
+    res = None
+    for i in range(args.steps):
+        res = agg.run_round(secrets)
+        verify(res, f"step {i}")
+    comm.barrier()
+    elapsed = comm.all_reduce_max(time.perf_counter() - t0)
+    ms = elapsed / max(1, args.steps) * 1e3
+    sent = comm.bytes_sent() / max(1, args.steps)
+    if rank == 0:
+        value = P * world * args.dim / (ms / 1e3)
+        print(json.dumps({
+            "metric": METRIC, "value": value, "unit": "elements/s", "n_gpus": 0, "ranks": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "int64 (host engines)", "data": "synthetic uniform random participant vectors",
+            "rehearsal": "CPU engines over gloo: exercises the launcher and the committee "
+                         "dataflow, not the benchmark",
+            "xgmi": {"bytes_sent_per_rank_per_round": sent, "rank": rank},
+            "config": {"model": f"SDA round: additive-{args.clerks} sharing, mod {m}, host engines",
+                       "global_batch": P * world, "seq_len": args.dim,
+                       "parallelism": f"dp{world} committee over gloo (CPU)"}}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    from sda_amd.utils.launch import self_launch, wants_self_launch
+
+    if wants_self_launch(args.gpus):
+        # asked for N ranks from a plain command line: start them as child processes
+        # (this parent has not imported torch and never touches a GPU)
+        sys.exit(self_launch(os.path.abspath(__file__), sys.argv[1:], args.gpus))
+    if args.engine == "host":
+        return host_rehearsal(args)
     if args.hw_queues > 0:  # must precede HIP init
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("bench.py: launch with torch.distributed.run for --gpus > 1", file=sys.stderr)
-            sys.exit(2)
+    world, rank, local_rank = launcher_env(args)
+    if args.loopback and not (args.force_dist and world == 1):
+        print("bench.py: --loopback needs --force-dist on one rank", file=sys.stderr)
+        sys.exit(2)
     dev_index = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_index)
     dist_mode = world > 1 or args.force_dist
@@ -161,7 +256,8 @@ def main():
         agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", dev_index),
                                     time_stages=args.stages, layout=args.layout,
                                     waves=waves, force_pipeline=args.force_dist,
-                                    deadline_s=min(60.0, args.dist_timeout / 4))
+                                    deadline_s=min(60.0, args.dist_timeout / 4),
+                                    loopback=args.loopback)
         engine, comm = agg.engine, agg.comm
         if not args.waves and world > 1 and args.layout == "committee":
             # untimed: pick the pipeline depth on this node's measured exchange rate
@@ -258,7 +354,10 @@ def main():
             parallelism = (f"dp{world} participants x committee-sharded clerks: all-to-all of "
                            f"sealed boxes over xGMI (grouped RCCL send/recv, {waves} waves), "
                            "per-rank key custody, sealed clerk results gathered on rank 0")
-            if world == 1:
+            if world == 1 and args.loopback:
+                parallelism += (" [one rank, loopback: its own piece travels through RCCL "
+                                "send/recv to itself; nothing crosses xGMI]")
+            elif world == 1:
                 parallelism += " [distributed engine on one rank: nothing crosses xGMI]"
         else:
             parallelism = (f"dp{world} owner (non-private upper bound): every GPU opens its own "

@@ -14,7 +14,8 @@ JSON line each (rank 0).
   --config 7  config 5 over a prime below 256 (u8 share storage)
   --config 8  16 x 1M per GPU, the reference's PSS_155_19682_100 (19,682 clerks)
 
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench_configs.py --config 3
+Multi-GPU: python bench_configs.py --config 3 --gpus N   (starts its own N ranks), or
+           python -m torch.distributed.run --nproc-per-node N bench_configs.py --config 3 --gpus N
 Scaled-down runs: --participants / --dim override the per-rank sizes;
 --pss-backend valu|mfma forces the packed-Shamir kernel family.
 """
@@ -36,6 +37,10 @@ if ROOT not in sys.path:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, required=True, choices=[1, 2, 3, 4, 5, 6, 7, 8])
+    ap.add_argument("--gpus", type=int, default=0,
+                    help="ranks (one per GPU). > 1 from a plain command line: the script starts "
+                         "them itself through torch.distributed.run. 0 = whatever the launcher "
+                         "started (1 from a plain command line)")
     ap.add_argument("--pss-backend", default=None, choices=["auto", "valu", "mfma"])
     ap.add_argument("--participants", type=int, default=None, help="per rank")
     ap.add_argument("--dim", type=int, default=None)
@@ -110,6 +115,8 @@ def gpu_configs(args):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.gpus and args.gpus != world:
+        raise SystemExit(f"bench_configs.py: --gpus {args.gpus} but the launcher started {world}")
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -163,34 +170,50 @@ def gpu_configs(args):
         secs = time.perf_counter() - t0
         if world > 1:
             secs = agg.comm.all_reduce_max(secs)
-        if args.check and world == 1:
+        if args.check:
             ref = torch.zeros(D, dtype=torch.int64, device=dev)
             for w in range((P + wave - 1) // wave):
                 ref += make(w, w * wave, min(wave, P - w * wave)).to(torch.int64).sum(0)
-            ok = bool(torch.equal(res.output, torch.remainder(ref, m).to(torch.int32)))
+            if world > 1:  # every rank's participants: the plain sums reduced to rank 0
+                ref = agg.comm.reduce_sum(ref)
+            if rank == 0:
+                ok = bool(torch.equal(res.output, torch.remainder(ref, m).to(torch.int32)))
         steps, ms = 1, secs * 1e3
     else:
         x = gen(1234 + rank, P)
 
-        def step():
+        def step(check):
             if world > 1:
-                return agg.run_round(x, clerks=clerks)
-            return eng.run_round(x, clerks=clerks)
-        for _ in range(args.warmup):
-            res = step()
+                return agg.run_round(x, clerks=clerks, check=check)
+            return eng.run_round(x, clerks=clerks, check=check)
+        # warm-up: checked rounds (at least one, so every kernel's code object is loaded
+        # and there is an output to verify), plus the timed loop's own device ops
+        err_total = torch.zeros(1, dtype=torch.int32, device=dev)
+        for _ in range(max(1, args.warmup)):
+            res = step(True)
+            err_total |= res.err
         if args.check:
             local_sum = x.to(torch.int64).sum(0)
             tot = agg.comm.reduce_sum(local_sum) if world > 1 else local_sum
             if rank == 0:
                 ok = bool(torch.equal(res.output, torch.remainder(tot, m).to(torch.int32)))
+        err_total.zero_()
         sync()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            res = step()
+            res = step(False)        # no host synchronisation inside the timed loop:
+            err_total |= res.err     # the error words are OR-ed on the device, read once
         sync()
         secs = time.perf_counter() - t0
+        e = int(err_total.item())
         if world > 1:
             secs = agg.comm.all_reduce_max(secs)
+            e = agg.comm.all_reduce_or(e)
+        if e:
+            from sda_amd.engine import describe_error
+
+            raise SystemExit(f"bench_configs: device error word 0x{e:x} in the timed steps "
+                             f"({describe_error(e)})")
         steps, ms = args.steps, secs / args.steps * 1e3
     if rank == 0:
         emit({"config": c, "name": cfg.name, "what": cfg.what,
@@ -213,8 +236,14 @@ def main():
     args = parse()
     if args.config == 1:
         config1()
-    else:
-        gpu_configs(args)
+        return
+    from sda_amd.utils.launch import self_launch, wants_self_launch
+
+    if wants_self_launch(args.gpus):
+        # N ranks asked for from a plain command line: child processes, started before
+        # this one has imported torch or touched a GPU
+        sys.exit(self_launch(os.path.abspath(__file__), sys.argv[1:], args.gpus))
+    gpu_configs(args)
 
 
 if __name__ == "__main__":

@@ -31,7 +31,9 @@ import torch.distributed as dist
 
 
 class Comm:
-    def __init__(self, group=None, deadline_s: float = 60.0):
+    _instances = 0  # per process: every rank constructs its Comm objects in the same order
+
+    def __init__(self, group=None, deadline_s: float = 60.0, loopback: bool = False):
         if not dist.is_initialized():
             raise RuntimeError("torch.distributed is not initialised")
         self.group = group
@@ -43,6 +45,17 @@ class Comm:
         self.audit: List[tuple] = []
         self.rendezvous_s = 0.0  # host time spent in the store rendezvous (arrive / decide / decision)
         self._store = None
+        # Rendezvous keys live under a per-instance prefix: round counters restart
+        # at 1 in every engine, and a second engine on the same process group must
+        # not read the first one's flags and decisions.
+        Comm._instances += 1
+        self._nonce = Comm._instances
+        self._garbage: List[tuple] = []  # (delete-after time, keys) of decisions this rank published
+        # Loopback: a rank's own piece of an exchange is sent to itself through the
+        # backend's send/recv instead of being copied locally. It makes the
+        # point-to-point path (grouped isend/irecv, the transfer stream's ordering
+        # against the compute streams) run on a single rank.
+        self.loopback = bool(loopback)
 
     # -- accounting -------------------------------------------------------------
     def note(self, kind: str, direction: str, peer: int, clerk: int, nbytes: int):
@@ -125,8 +138,8 @@ class Comm:
         """Start a point-to-point exchange; returns a handle with ``wait()``.
 
         `sends` / `recvs` are lists of (peer, tensor); transfers between one
-        pair of ranks are matched in list order; peer == self must not appear
-        (callers copy locally). With RCCL the operations are one grouped launch
+        pair of ranks are matched in list order; peer == self appears only in
+        loopback mode (callers otherwise copy locally). With RCCL the operations are one grouped launch
         on the communicator's stream (every xGMI link busy at once), which
         first waits for work already queued on the current stream; the caller
         keeps queuing compute and calls ``wait()`` (the current stream then
@@ -146,12 +159,22 @@ class Comm:
         self.exchange_async(sends, recvs).wait()
 
     def _exchange_host(self, sends, recvs):
+        # gloo has no pair from a rank to itself: loopback transfers are matched in
+        # list order here (RCCL carries them as real send/recv pairs)
+        own_s = [t for p, t in sends if p == self.rank]
+        own_r = [t for p, t in recvs if p == self.rank]
+        if len(own_s) != len(own_r):
+            raise RuntimeError("loopback: unmatched transfers to self")
+        for src, dst in zip(own_s, own_r):
+            dst.copy_(src)
+        sends = [(p, t) for p, t in sends if p != self.rank]
+        recvs = [(p, t) for p, t in recvs if p != self.rank]
         host_sends = [(p, t.contiguous().cpu() if t.is_cuda else t.contiguous()) for p, t in sends]
         host_recvs = [(p, torch.empty(t.shape, dtype=t.dtype) if (t.is_cuda or not t.is_contiguous())
                        else t, t) for p, t in recvs]
         ops = [dist.P2POp(dist.isend, t, p, group=self.group) for p, t in host_sends]
         ops += [dist.P2POp(dist.irecv, h, p, group=self.group) for p, h, _ in host_recvs]
-        for w in dist.batch_isend_irecv(ops):
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
             w.wait()
         for _, h, t in host_recvs:
             if h is not t:
@@ -181,7 +204,7 @@ class Comm:
         if self._store is None:
             from torch.distributed.distributed_c10d import _get_default_store
 
-            self._store = dist.PrefixStore("sda", _get_default_store())
+            self._store = dist.PrefixStore(f"sda{self._nonce}", _get_default_store())
         return self._store
 
     def arrive(self, topic: str, who) -> None:
@@ -211,8 +234,23 @@ class Comm:
             live = []
         pub = [str(w) for w in live] + [str(w) for w in also]
         self.store.set(f"{topic}/live", ",".join(pub).encode() or b"-")
+        self._collect(list(keys.values()) + [f"{topic}/live"])
         self.rendezvous_s += time.perf_counter() - t0
         return live
+
+    def _collect(self, keys: List[str]) -> None:
+        """Delete the keys of decisions that every reader has given up on or read by
+        now (a reader waits at most 3 deadlines + 2 s), so the store does not grow by
+        O(clerks) keys per round."""
+        now = time.monotonic()
+        self._garbage.append((now + 4 * self.deadline_s + 10, keys))
+        while self._garbage and self._garbage[0][0] < now:
+            for k in self._garbage.pop(0)[1]:
+                try:
+                    self.store.delete_key(k)
+                except Exception:  # noqa: BLE001 - a store without delete support only grows
+                    self._garbage.clear()
+                    return
 
     def decision(self, topic: str, deadline_s: Optional[float] = None) -> List[str]:
         """The published outcome of :meth:`decide`. Blocks until it is there; a

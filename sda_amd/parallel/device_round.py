@@ -39,10 +39,13 @@ from .liveness import partial_stage, result_stage
 from .routing import hosted_clerks, hosts, lead, plan
 
 
-def _header_arena(hdr: torch.Tensor) -> Arena:
+def _header_arena(hdr: torch.Tensor, K: int) -> Arena:
     """32-byte ephemeral public keys [M][32] viewed as an arena of bare headers
-    (all that key agreement reads)."""
-    return Arena(hdr.shape[0], 0, 0, 32, 0, hdr.view(-1), None)
+    (all that key agreement reads). `K`: chunks per slot of the arena the boxes
+    themselves live in -- it decides whether the derived key set carries the
+    complete Poly1305 tables, so that they are made here, beside the bulk work,
+    and not again on the consuming stream."""
+    return Arena(hdr.shape[0], 0, 0, 32, K, hdr.view(-1), None)
 
 
 @dataclass
@@ -141,16 +144,17 @@ class DeviceCommittee:
             hdr_in = None
             if me == root:
                 hdr_in = torch.zeros(len(live), 32, dtype=torch.uint8, device=dev)
+            loop = comm.loopback
             for i, c in enumerate(live):
                 ld = lead(c, comm.world, n)
                 if ld == me:
                     row = hdr[ctx.led.index(c):ctx.led.index(c) + 1]
-                    if me == root:
+                    if me == root and not loop:
                         hdr_in[i:i + 1].copy_(row)
                     else:
                         sends.append((root, row))
                         comm.note("hdr", "send", root, c, 32)
-                elif me == root:
+                if me == root and (ld != me or loop):
                     recvs.append((ld, hdr_in[i:i + 1]))
                     comm.note("hdr", "recv", ld, c, 32)
             h = comm.exchange_async(sends, recvs)
@@ -158,8 +162,8 @@ class DeviceCommittee:
             if me == root:
                 ctx.res_in = Arena.empty(len(live), B, m, dev)
                 kidx_r = torch.full((len(live),), n, dtype=torch.int32, device=dev)
-                ctx.ko_res = open_setup(_header_arena(hdr_in), kidx_r, sks, pks, err)
-                if comm.world == 1 and ctx.led == list(live):
+                ctx.ko_res = open_setup(_header_arena(hdr_in, ctx.res_in.K), kidx_r, sks, pks, err)
+                if comm.world == 1 and ctx.led == list(live) and not loop:
                     ctx.res_in = ctx.res_arena  # one rank: the results are opened where they were sealed
             ctx.ev = torch.cuda.Event()
             ctx.ev.record(side)
@@ -215,7 +219,7 @@ class DeviceCommittee:
 
         # wave-blocked clerk-major arena: wave w's n * P_w slots are contiguous
         arena = Arena.empty(n * P, B, m, dev)
-        alias = W == 1  # one rank: the inbox is the arena, nothing moves
+        alias = W == 1 and not comm.loopback  # one rank: the inbox is the arena, nothing moves
         kidx_send = torch.cat([eng._kidx_clerk(hi - lo) for lo, hi in bounds])
         if alias:
             inbox, kidx_in = arena, kidx_send
@@ -253,7 +257,7 @@ class DeviceCommittee:
                     recvs += r_
                 h = comm.exchange_async(sends, recvs)
                 h.wait()
-                ko = open_setup(_header_arena(hdr_in), kidx_in, sks, pks, err)
+                ko = open_setup(_header_arena(hdr_in, arena.K), kidx_in, sks, pks, err)
             ev_open = torch.cuda.Event()
             ev_open.record(side)
         # caching-allocator stream bookkeeping: side-allocated keys are consumed on
@@ -340,7 +344,7 @@ class DeviceCommittee:
         eng, comm = self.engine, self.comm
         W, me, root, dev = comm.world, comm.rank, self.ROOT, eng.device
         P = mask_arena.M
-        if W == 1:
+        if W == 1 and not comm.loopback:
             box = mask_arena
         else:
             box = None
@@ -427,18 +431,19 @@ class DeviceCommittee:
                 if c not in arrived:
                     continue
                 ld = lead(c, W, n)
+                loop = comm.loopback
                 if ld == me:
                     k = ctx.led.index(c)
                     src = ctx.res_arena.ct.view(-1, ctx.res_arena.stride)[k:k + 1]
                     srcl = ctx.res_arena.pt_len.view(-1, 1)[k:k + 1]
-                    if me == root:
+                    if me == root and not loop:
                         if ctx.res_in is not ctx.res_arena:
                             ctx.res_in.ct.view(-1, ctx.res_in.stride)[i:i + 1].copy_(src)
                             ctx.res_in.pt_len.view(-1, 1)[i:i + 1].copy_(srcl)
                     else:
                         sends += [(root, src), (root, srcl)]
                         comm.note("result", "send", root, c, src.numel())
-                elif me == root:
+                if me == root and (ld != me or loop):
                     recvs += [(ld, ctx.res_in.ct.view(-1, ctx.res_in.stride)[i:i + 1]),
                               (ld, ctx.res_in.pt_len.view(-1, 1)[i:i + 1])]
                     comm.note("result", "recv", ld, c, ctx.res_in.stride)

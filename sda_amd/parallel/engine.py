@@ -62,13 +62,14 @@ class DistributedAggregator:
     def __init__(self, spec: AggregationSpec, engine: str = "device", device=None, group=None,
                  time_stages: bool = False, layout: str = "committee", waves: int = 4,
                  force_pipeline: bool = False, fault_tolerant: bool = True,
-                 deadline_s: float = 60.0, fault_hook=None, pss_backend: str = "auto"):
+                 deadline_s: float = 60.0, fault_hook=None, pss_backend: str = "auto",
+                 loopback: bool = False):
         if layout not in ("committee", "owner"):
             raise ValueError("layout must be 'committee' or 'owner'")
         if engine not in ("device", "host"):
             raise ValueError("engine must be 'device' or 'host'")
         self.spec = spec
-        self.comm = Comm(group, deadline_s=deadline_s)
+        self.comm = Comm(group, deadline_s=deadline_s, loopback=loopback)
         self.rank, self.world = self.comm.rank, self.comm.world
         self.kind, self.layout = engine, layout
         self.fault_tolerant, self.fault_hook = fault_tolerant, fault_hook

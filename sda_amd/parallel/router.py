@@ -32,12 +32,13 @@ class RowRouter:
         Returns (sends, recvs) for :meth:`Comm.exchange_async`.
         """
         me = self.comm.rank
+        loop = self.comm.loopback  # the own piece travels like any other
         sends, recvs = [], []
         for t in self.plan.sends:
             if t.count == 0:
                 continue
             s = slice(src_base + t.src_row, src_base + t.src_row + t.count)
-            if t.peer == me:
+            if t.peer == me and not loop:
                 d = slice(dst_base + t.dst_row, dst_base + t.dst_row + t.count)
                 for src, dst in pairs:
                     if dst.data_ptr() != src.data_ptr() or s != d:
@@ -48,7 +49,7 @@ class RowRouter:
                 sends.append((t.peer, rows))
                 self.comm.note(kind, "send", t.peer, t.clerk, rows.numel() * rows.element_size())
         for t in self.plan.recvs:
-            if t.count == 0 or t.peer == me:
+            if t.count == 0 or (t.peer == me and not loop):
                 continue
             d = slice(dst_base + t.dst_row, dst_base + t.dst_row + t.count)
             for _, dst in pairs:
@@ -64,11 +65,12 @@ def gather_rows_to(comm: Comm, root: int, pairs: Iterable[Tuple[torch.Tensor, to
     each `src` to `root`, which places rank r's at rows [r * rows_per_rank, ...)
     of `dst`. Returns (sends, recvs)."""
     me = comm.rank
+    loop = comm.loopback
     senders = list(range(comm.world)) if senders is None else list(senders)
     sends, recvs = [], []
     for src, dst in pairs:
         if me in senders:
-            if me == root:
+            if me == root and not loop:
                 dst[me * rows_per_rank:(me + 1) * rows_per_rank].copy_(src[:rows_per_rank])
             else:
                 rows = src[:rows_per_rank]
@@ -76,7 +78,7 @@ def gather_rows_to(comm: Comm, root: int, pairs: Iterable[Tuple[torch.Tensor, to
                 comm.note(kind, "send", root, -1, rows.numel() * rows.element_size())
         if me == root:
             for r in senders:
-                if r != root:
+                if r != root or loop:
                     rows = dst[r * rows_per_rank:(r + 1) * rows_per_rank]
                     recvs.append((r, rows))
                     comm.note(kind, "recv", r, -1, rows.numel() * rows.element_size())

@@ -142,3 +142,71 @@ def test_bench_fails_on_a_corrupted_box_in_a_timed_step(cuda, dist):
     assert out.returncode != 0
     assert "MAC verification failed" in out.stderr, out.stderr[-2000:]
     assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_loopback_over_rccl(cuda):
+    """One rank, `nccl` group, loopback: the rank's own piece of the header
+    exchange (side stream), of every wave's box exchange and of the result path
+    travels through grouped RCCL isend/irecv to itself, so the point-to-point path
+    and its stream ordering against the compute streams run on a one-GPU machine.
+    The process-group timeout is short: a self send/recv that RCCL cannot match
+    fails the test instead of hanging it."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "1", "--force-dist",
+           "--loopback", "--waves", "3", "--dist-timeout", "60", "--steps", "2", "--warmup", "1",
+           "--participants", "48", "--dim", "100000", "--check"]
+    out = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=200)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0 and "loopback" in line["config"]["parallelism"]
+
+
+def _loopback_worker(port, name, q):
+    import datetime
+
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0),
+                                timeout=datetime.timedelta(seconds=60))
+        from sda_amd.models.schemes import PSS_4_8_3, Additive, AggregationSpec, FullMask
+        from sda_amd.parallel import DistributedAggregator
+
+        D, P, m = 5000, 12, 433
+        spec = {"fullmask": AggregationSpec(D, m, Additive(3, m), FullMask(m)),
+                "pss": AggregationSpec(D, m, PSS_4_8_3)}[name]
+        agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", 0),
+                                    waves=3, force_pipeline=True, deadline_s=15.0, loopback=True)
+        x = torch.randint(0, m, (P, D), dtype=torch.int32, device="cuda")
+        ok = True
+        for _ in range(3):  # several rounds: send buffers and events are recycled
+            res = agg.run_round(x)
+            ok = ok and bool(torch.equal(res.output.cpu().to(torch.int64),
+                                         torch.remainder(x.cpu().to(torch.int64).sum(0), m)))
+        sent = sorted({k for k, d, *_ in agg.comm.audit if d == "send"})
+        q.put(("ok", ok, sent))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", f"{type(e).__name__}: {e}", []))
+
+
+@pytest.mark.parametrize("name", ["fullmask", "pss"])
+def test_loopback_rounds_with_masks_and_pss_over_rccl(cuda, name):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_loopback_worker, args=(_free_port(), name, q))
+    p.start()
+    kind, ok, sent = q.get(timeout=200)
+    p.join(timeout=60)
+    assert kind == "ok" and ok, (kind, ok)
+    # everything that would cross xGMI went through send/recv: headers, boxes, results
+    assert {"hdr", "box", "result"} <= set(sent), sent
+    if name == "fullmask":
+        assert "mask" in sent
