@@ -123,6 +123,9 @@ def parse():
                          "(ephemeral-key headers, sealed boxes, result boxes) goes through an RCCL "
                          "send/recv to itself instead of a local copy, so the point-to-point path "
                          "and its stream ordering run on a one-GPU machine")
+    ap.add_argument("--p2p-chunk-mb", type=int, default=1024,
+                    help="largest single RCCL send/recv; longer transfers are cut into runs of "
+                         "whole boxes")
     ap.add_argument("--corrupt-step", type=int, default=-1,
                     help="fault injection: flip a ciphertext bit in this timed step (the run must fail)")
     return ap.parse_args()
@@ -257,7 +260,8 @@ def main():
                                     time_stages=args.stages, layout=args.layout,
                                     waves=waves, force_pipeline=args.force_dist,
                                     deadline_s=min(60.0, args.dist_timeout / 4),
-                                    loopback=args.loopback)
+                                    loopback=args.loopback,
+                                    max_op_bytes=args.p2p_chunk_mb << 20)
         engine, comm = agg.engine, agg.comm
         if not args.waves and world > 1 and args.layout == "committee":
             # untimed: pick the pipeline depth on this node's measured exchange rate
@@ -393,6 +397,7 @@ def main():
                                  "note": "rank 0's host time inside run_round; the GPU runs behind "
                                          "it, so it only bounds the step when it exceeds ms_per_step"},
             "pipeline_waves": waves if dist_mode else None,
+            "compute_stream_vs_rccl": comm.compute_stream_probe if dist_mode else None,
             "pipeline_wave_tuning_ms": {str(k): v for k, v in wave_tuning.items()} or None,
             "timed_steps_verified": "device error word of every timed step (OR over steps and "
                                     "ranks) + last round's output vs the plain sum",

@@ -33,7 +33,8 @@ import torch.distributed as dist
 class Comm:
     _instances = 0  # per process: every rank constructs its Comm objects in the same order
 
-    def __init__(self, group=None, deadline_s: float = 60.0, loopback: bool = False):
+    def __init__(self, group=None, deadline_s: float = 60.0, loopback: bool = False,
+                 max_op_bytes: int = 1 << 30):
         if not dist.is_initialized():
             raise RuntimeError("torch.distributed is not initialised")
         self.group = group
@@ -56,6 +57,11 @@ class Comm:
         # point-to-point path (grouped isend/irecv, the transfer stream's ordering
         # against the compute streams) run on a single rank.
         self.loopback = bool(loopback)
+        # Largest single send/recv: longer transfers are cut into runs of whole rows
+        # (both sides cut alike, the shapes agree), which also keeps every op's byte
+        # count far below 2^31.
+        self.max_op_bytes = int(max_op_bytes)
+        self.compute_stream_probe = None  # outcome of pick_compute_stream, for reports
 
     # -- accounting -------------------------------------------------------------
     def note(self, kind: str, direction: str, peer: int, clerk: int, nbytes: int):
@@ -151,12 +157,78 @@ class Comm:
         if not self.device_native:
             self._exchange_host(sends, recvs)
             return _Done()
-        ops = [dist.P2POp(dist.isend, t.contiguous(), p, group=self.group) for p, t in sends]
+        sends = [(p, c) for p, t in sends for c in self._cut(t.contiguous())]
+        recvs = [(p, c) for p, t in recvs for c in self._cut(t)]
+        ops = [dist.P2POp(dist.isend, t, p, group=self.group) for p, t in sends]
         ops += [dist.P2POp(dist.irecv, t, p, group=self.group) for p, t in recvs]
         return _Pending(dist.batch_isend_irecv(ops), [t for _, t in sends])
 
+    def _cut(self, t: torch.Tensor):
+        """`t` as runs of whole leading-dimension rows of at most max_op_bytes each."""
+        nbytes = t.numel() * t.element_size()
+        if nbytes <= self.max_op_bytes or t.dim() == 0 or t.shape[0] <= 1:
+            return [t]
+        if not t.is_contiguous():
+            raise ValueError("exchange: receive buffers must be contiguous")
+        row = nbytes // t.shape[0]
+        step = max(1, self.max_op_bytes // max(1, row))
+        return [t[i:i + step] for i in range(0, t.shape[0], step)]
+
     def exchange(self, sends, recvs):
         self.exchange_async(sends, recvs).wait()
+
+    def pick_compute_stream(self, device, tries: int = 8, spin_us: int = 1500):
+        """A stream whose kernels run *beside* the backend's transfers.
+
+        HIP multiplexes a process's streams onto few hardware queues (4 by
+        default) and two streams on one queue serialise. RCCL launches its
+        transfer kernels on a stream of its own; if that stream shares a queue
+        with the stream the round's kernels are queued on, every wave's exchange
+        runs behind the next wave's compute instead of beside it (seen in a
+        kernel trace: transfer kernels and compute kernels on one queue id, back
+        to back). Candidates are probed: the candidate runs a bounded spin (a
+        gate the host never posts), the backend carries a small send/recv of
+        this rank to itself, issued from another stream; a candidate whose spin
+        is still running when the transfer has finished sits on another queue.
+        Every rank probes for itself (the transfer is local), no rank waits for
+        another. Falls back to the current stream on any failure: correct,
+        only without the overlap."""
+        dev = torch.device(device)
+        cur = torch.cuda.current_stream(dev)
+        if not self.device_native:
+            return cur
+        try:
+            from ..ops import gpu as G
+
+            gate = torch.zeros(1, dtype=torch.int32, device=dev)
+            src = torch.zeros(4 << 20, dtype=torch.uint8, device=dev)
+            dst = torch.empty_like(src)
+            issue = torch.cuda.Stream(device=dev)
+            cand = cur
+            with torch.cuda.device(dev):
+                for _ in range(tries):
+                    cand = torch.cuda.Stream(device=dev)
+                    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                    torch.cuda.synchronize(dev)
+                    with torch.cuda.stream(cand):
+                        e0.record(cand)
+                        G.gate_wait((gate, 1), timeout_us=spin_us)  # never posted: ends at the limit
+                        e2.record(cand)
+                    with torch.cuda.stream(issue):
+                        ops = [dist.P2POp(dist.isend, src, self.rank, group=self.group),
+                               dist.P2POp(dist.irecv, dst, self.rank, group=self.group)]
+                        for w in dist.batch_isend_irecv(ops):
+                            w.wait()
+                        e1.record(issue)
+                    torch.cuda.synchronize(dev)
+                    if e0.elapsed_time(e1) < 0.6 * e0.elapsed_time(e2):
+                        self.compute_stream_probe = "beside the transfers"
+                        return cand
+            self.compute_stream_probe = "no candidate ran beside the transfers"
+            return cand
+        except Exception as e:  # noqa: BLE001 - the probe is an optimisation only
+            self.compute_stream_probe = f"probe failed: {type(e).__name__}"
+            return cur
 
     def _exchange_host(self, sends, recvs):
         # gloo has no pair from a rank to itself: loopback transfers are matched in

@@ -63,16 +63,18 @@ class DistributedAggregator:
                  time_stages: bool = False, layout: str = "committee", waves: int = 4,
                  force_pipeline: bool = False, fault_tolerant: bool = True,
                  deadline_s: float = 60.0, fault_hook=None, pss_backend: str = "auto",
-                 loopback: bool = False):
+                 loopback: bool = False, max_op_bytes: int = 1 << 30):
         if layout not in ("committee", "owner"):
             raise ValueError("layout must be 'committee' or 'owner'")
         if engine not in ("device", "host"):
             raise ValueError("engine must be 'device' or 'host'")
         self.spec = spec
-        self.comm = Comm(group, deadline_s=deadline_s, loopback=loopback)
+        self.comm = Comm(group, deadline_s=deadline_s, loopback=loopback,
+                         max_op_bytes=max_op_bytes)
         self.rank, self.world = self.comm.rank, self.comm.world
         self.kind, self.layout = engine, layout
         self.fault_tolerant, self.fault_hook = fault_tolerant, fault_hook
+        self.stream = None
         n = spec.n_clerks
         self.hosted = hosted_clerks(self.rank, self.world, n) if layout == "committee" \
             else list(range(n))
@@ -86,6 +88,13 @@ class DistributedAggregator:
                                            keys=KeyTable.from_bytes(pk, sk, device),
                                            time_stages=time_stages, pss_backend=pss_backend)
             self._committee = None
+            # the round's kernels go on a stream that does not share a hardware
+            # queue with RCCL's transfer stream (committee layout: the exchange of
+            # wave w must run beside the sealing of wave w + 1)
+            if layout == "committee" and self.comm.device_native and \
+                    (self.world > 1 or loopback):
+                with torch.cuda.device(device):
+                    self.stream = self.comm.pick_compute_stream(device)
             if layout == "committee":
                 from .device_round import DeviceCommittee
 
@@ -174,6 +183,20 @@ class DistributedAggregator:
                                          reducer=self._reduce, owner_base=_owner_base(self.rank))
         if self.kind == "host":
             return self._host_round(secrets_local, clerks)
+        if self.stream is None:
+            return self._committee_round(secrets_local, clerks, check)
+        # on the probed compute stream, ordered after and before the caller's stream
+        caller = torch.cuda.current_stream(self.engine.device)
+        self.stream.wait_stream(caller)
+        with torch.cuda.stream(self.stream):
+            res = self._committee_round(secrets_local, clerks, check)
+        caller.wait_stream(self.stream)
+        for t in (res.output, res.err):
+            if t is not None:
+                t.record_stream(caller)
+        return res
+
+    def _committee_round(self, secrets_local, clerks, check):
         from ..engine import RoundResult
 
         eng, cm = self.engine, self._committee
@@ -208,8 +231,18 @@ class DistributedAggregator:
         if self.layout == "owner":
             return st.run(total_local, make_wave, clerks=clerks, reducer=self._reduce,
                           owner_base=_owner_base(self.rank), resume=resume)
-        return st.run(total_local, make_wave, clerks=clerks, committee=self._committee,
-                      owner_base=_owner_base(self.rank), resume=resume)
+        if self.stream is None:
+            return st.run(total_local, make_wave, clerks=clerks, committee=self._committee,
+                          owner_base=_owner_base(self.rank), resume=resume)
+        caller = torch.cuda.current_stream(self.engine.device)
+        self.stream.wait_stream(caller)
+        with torch.cuda.stream(self.stream):
+            res = st.run(total_local, make_wave, clerks=clerks, committee=self._committee,
+                         owner_base=_owner_base(self.rank), resume=resume)
+        caller.wait_stream(self.stream)
+        if res.output is not None:
+            res.output.record_stream(caller)
+        return res
 
     # ---- committee round on the host engines (CPU, gloo) ----------------------------
     def _hook(self, stage: str):
