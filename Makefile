@@ -7,11 +7,14 @@
 # Outputs (in-tree, git-ignored, shipped to the GPU box with the snapshot):
 #   sda_amd/_lib/_sda_native<EXT>   host control plane + crypto bindings
 #   sda_amd/_lib/_sda_gpu<EXT>      HIP/CDNA4 kernels (hipcc --offload-arch=gfx950)
+#   sda_amd/_lib/libsda_device.so   the client roles' GPU backend (kernels + C++ driver),
+#                                   loaded on demand by `sda --device gpu` and the Python client
 #   sda_amd/_lib/bin/sda, sdad      agent CLI and server daemon
 
 PYTHON   ?= python3
 CXX      ?= g++
-HIPCC    ?= /opt/rocm/bin/hipcc
+ROCM     ?= /opt/rocm
+HIPCC    ?= $(ROCM)/bin/hipcc
 GPU_ARCH ?= gfx950
 
 EXT        := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
@@ -43,12 +46,13 @@ HIP_BIND := csrc/kernels/gpu_module.cpp
 
 NATIVE_MOD := $(LIB)/_sda_native$(EXT)
 GPU_MOD    := $(LIB)/_sda_gpu$(EXT)
+DEVICE_LIB := $(LIB)/libsda_device.so
 BINS       := $(patsubst csrc/bin/%.cc,$(BIN)/%,$(wildcard csrc/bin/*.cc))
 
-.PHONY: all host gpu clean asan tsan selftest emul
+.PHONY: all host gpu clean asan tsan selftest emul check
 all: host gpu
 host: $(NATIVE_MOD) $(BINS)
-gpu: $(GPU_MOD)
+gpu: $(GPU_MOD) $(DEVICE_LIB)
 
 $(BUILD)/core/%.o: csrc/src/%.cc $(wildcard csrc/include/sda/*.hpp)
 	@mkdir -p $(dir $@)
@@ -64,11 +68,11 @@ $(BUILD)/py/%.o: csrc/python/%.cc $(wildcard csrc/include/sda/*.hpp)
 
 $(NATIVE_MOD): $(PY_OBJ) $(CORE_LIB)
 	@mkdir -p $(dir $@)
-	$(CXX) -shared -o $@ $(PY_OBJ) $(CORE_LIB) -pthread
+	$(CXX) -shared -o $@ $(PY_OBJ) $(CORE_LIB) -pthread -ldl
 
 $(BIN)/%: csrc/bin/%.cc $(CORE_LIB)
 	@mkdir -p $(dir $@)
-	$(CXX) $(CXXFLAGS) $(INCS) $< $(CORE_LIB) -o $@ -pthread
+	$(CXX) $(CXXFLAGS) $(INCS) $< $(CORE_LIB) -o $@ -pthread -ldl
 
 $(BUILD)/hip/%.o: csrc/kernels/%.hip $(wildcard csrc/kernels/*.hpp) $(wildcard csrc/include/sda/*.hpp)
 	@mkdir -p $(dir $@)
@@ -80,7 +84,16 @@ $(BUILD)/hip/gpu_module.o: $(HIP_BIND) $(wildcard csrc/kernels/*.hpp) $(wildcard
 
 $(GPU_MOD): $(HIP_OBJ) $(BUILD)/hip/gpu_module.o $(CORE_LIB)
 	@mkdir -p $(dir $@)
-	$(HIPCC) -shared --offload-arch=$(GPU_ARCH) -o $@ $^ -pthread
+	$(HIPCC) -shared --offload-arch=$(GPU_ARCH) -o $@ $^ -pthread -ldl
+
+# the roles' GPU backend: host C++ driving the same kernel objects
+$(BUILD)/hip/device_backend.o: csrc/device/device_backend.cc $(wildcard csrc/kernels/*.hpp) $(wildcard csrc/include/sda/*.hpp)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -Wno-unused-result -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include $(INCS) -c $< -o $@
+
+$(DEVICE_LIB): $(HIP_OBJ) $(BUILD)/hip/device_backend.o $(CORE_LIB)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -shared --offload-arch=$(GPU_ARCH) -o $@ $^ -pthread -ldl
 
 # sanitizer builds of the host control plane; run the C++ self-test
 asan: $(BUILD)/asan/sda_selftest
@@ -89,18 +102,26 @@ $(BUILD)/asan/sda_selftest: csrc/bin/sda_selftest.cc $(CORE_SRC) $(wildcard csrc
 	@mkdir -p $(BUILD)/asan
 	$(CXX) -O1 -g -std=c++17 -fsanitize=address,undefined -fno-sanitize-recover=undefined \
 	    -fno-omit-frame-pointer $(INCS) csrc/bin/sda_selftest.cc $(CORE_SRC) \
-	    -o $@ -pthread
+	    -o $@ -pthread -ldl
 tsan: $(BUILD)/tsan/sda_selftest
 	TSAN_OPTIONS=halt_on_error=1 $(BUILD)/tsan/sda_selftest
 $(BUILD)/tsan/sda_selftest: csrc/bin/sda_selftest.cc $(CORE_SRC) $(wildcard csrc/include/sda/*.hpp)
 	@mkdir -p $(BUILD)/tsan
 	$(CXX) -O1 -g -std=c++17 -fsanitize=thread -fno-omit-frame-pointer $(INCS) \
-	    csrc/bin/sda_selftest.cc $(CORE_SRC) -o $@ -pthread
+	    csrc/bin/sda_selftest.cc $(CORE_SRC) -o $@ -pthread -ldl
 selftest: $(BIN)/sda_selftest
 	$(BIN)/sda_selftest
 
 clean:
 	rm -rf $(BUILD) $(LIB)/*.so $(BIN)
+
+# one command for everything a checkout must pass without a GPU: build, the CPU test
+# suite (protocol, stores, REST, CLI walkthrough with an asserted output, crypto
+# KATs, gloo multi-process rounds), the sanitizer self-tests and the host emulation
+# of the device algorithms
+check: all
+	$(PYTHON) -m pytest tests -x -q -m "not gpu"
+	$(MAKE) asan tsan emul
 
 # host emulation of the device algorithms (no GPU needed)
 emul: $(BUILD)/hip/host_emul
@@ -108,4 +129,4 @@ emul: $(BUILD)/hip/host_emul
 $(BUILD)/hip/host_emul: csrc/kernels/host_emul.cpp $(wildcard csrc/kernels/*.hpp) $(CORE_LIB)
 	@mkdir -p $(dir $@)
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(GPU_ARCH) $(NO_PK_F32) $(INCS) -c $< -o $@.o
-	$(HIPCC) --offload-arch=$(GPU_ARCH) $@.o $(CORE_LIB) -o $@ -pthread
+	$(HIPCC) --offload-arch=$(GPU_ARCH) $@.o $(CORE_LIB) -o $@ -pthread -ldl

@@ -1,6 +1,6 @@
 // `sda` -- the agent command line (reference cli/src/main.rs).
 //
-//   sda [-s SERVER] [-i IDENTITY] [-v...] <command>
+//   sda [-s SERVER] [-i IDENTITY] [--device cpu|gpu[:N]] [-v...] <command>
 //     ping
 //     agent create [-f|--force] | agent show | agent keys create | agent keys show
 //     clerk [-o|--once] [--interval SECONDS]
@@ -9,6 +9,11 @@
 //                [--mask none|full|chacha] [--sharing add|shamir]
 //         begin ID | end ID | reveal ID
 //     participate ID VALUE...
+//     participate-file ID FILE        one vector per line (bulk; one participation each)
+//
+// `--device gpu` runs the bulk cryptography of clerk / reveal / participate on an
+// MI355X through libsda_device.so (loaded on demand; the wire format is
+// unchanged, so GPU and CPU agents mix freely in one aggregation).
 //
 // Identity layout (cli/src/main.rs:99-124): IDENTITY (default `.sda`) holds the
 // agent (alias `agent`) and the REST auth token; IDENTITY/keys holds the signing
@@ -22,6 +27,8 @@
 #include <cstdio>
 #include <cstring>
 #include <dirent.h>
+#include <fstream>
+#include <sstream>
 #include <string>
 #include <thread>
 #include <vector>
@@ -38,7 +45,7 @@ namespace {
 [[noreturn]] void usage(const std::string& why = "") {
   if (!why.empty()) std::fprintf(stderr, "error: %s\n\n", why.c_str());
   std::fprintf(stderr,
-               "usage: sda [-s SERVER] [-i IDENTITY] [-v...] <command>\n"
+               "usage: sda [-s SERVER] [-i IDENTITY] [--device cpu|gpu[:N]] [-v...] <command>\n"
                "  ping                          check service availability\n"
                "  agent create [-f]             create (or reuse) and upload the local agent\n"
                "  agent show                    show the local agent\n"
@@ -47,7 +54,9 @@ namespace {
                "  aggregations create TITLE DIMENSION MODULUS KEY SHARE_COUNT\n"
                "               [--id ID] [--mask none|full|chacha] [--sharing add|shamir]\n"
                "  aggregations begin|end|reveal ID\n"
-               "  participate ID VALUE...       contribute a vector\n");
+               "  participate ID VALUE...       contribute a vector\n"
+               "  participate-file ID FILE      contribute every line of FILE as a vector\n"
+               "  --device gpu[:N]              clerk / reveal / participate on MI355X N\n");
   std::exit(2);
 }
 
@@ -70,7 +79,7 @@ struct Args {
 // except negative numbers, which are values of `participate`).
 bool takes_value(const std::string& o) {
   return o == "-s" || o == "--server" || o == "-i" || o == "--identity" || o == "--id" ||
-         o == "--mask" || o == "--sharing" || o == "--interval";
+         o == "--mask" || o == "--sharing" || o == "--interval" || o == "--device";
 }
 
 bool is_number(const std::string& s) {
@@ -171,6 +180,20 @@ int run(const Args& a) {
     if (a.pos.size() <= i) usage(std::string("missing ") + what);
     return a.pos[i];
   };
+  // --device gpu[:N]: the roles' bulk cryptography on an MI355X
+  DeviceBackendPtr device;
+  const std::string dev = a.opt("--device", nullptr, "cpu");
+  if (dev.rfind("gpu", 0) == 0) {
+    int index = 0;
+    if (dev.size() > 3) {
+      if (dev[3] != ':' || !is_number(dev.substr(4))) usage("--device must be cpu, gpu or gpu:N");
+      index = std::stoi(dev.substr(4));
+    }
+    device = load_device_backend("", index);
+    log_info("Roles run on " + device->describe());
+  } else if (dev != "cpu" && dev != "host") {
+    usage("--device must be cpu, gpu or gpu:N");
+  }
 
   if (cmd == "ping") {
     if (!service->ping().running) throw SdaError("Service may not be running");
@@ -226,6 +249,7 @@ int run(const Args& a) {
     Agent ag = need_agent();
     service->ping();
     SdaClient client(ag, keystore, service);
+    client.set_device_backend(device);
     const long interval = std::stol(a.opt("--interval", nullptr, "300"));
     for (;;) {
       log_debug("Polling for clerking job");
@@ -238,6 +262,7 @@ int run(const Args& a) {
     Agent ag = need_agent();
     service->ping();
     SdaClient client(ag, keystore, service);
+    client.set_device_backend(device);
     const std::string sub = arg(1, "aggregations subcommand");
     if (sub == "create") {
       Aggregation agg;
@@ -302,7 +327,31 @@ int run(const Args& a) {
       if (!is_number(a.pos[i])) usage("not an integer: " + a.pos[i]);
       values.push_back(std::stoll(a.pos[i]));
     }
-    client.participate(values, id);
+    if (device) client.set_device_backend(device), client.participate_many({values}, id);
+    else client.participate(values, id);
+    return 0;
+  }
+  if (cmd == "participate-file") {
+    SdaClient client(need_agent(), keystore, service);
+    client.set_device_backend(device);
+    const AggregationId id = AggregationId::parse(arg(1, "aggregation id"));
+    std::ifstream in(arg(2, "file"));
+    if (!in) throw SdaError("cannot read " + a.pos[2]);
+    std::vector<std::vector<int64_t>> inputs;
+    std::string line;
+    while (std::getline(in, line)) {
+      std::istringstream ls(line);
+      std::vector<int64_t> v;
+      std::string tok;
+      while (ls >> tok) {
+        if (!tok.empty() && tok.back() == ',') tok.pop_back();
+        if (!is_number(tok)) throw SdaError("not an integer: " + tok);
+        v.push_back(std::stoll(tok));
+      }
+      if (!v.empty()) inputs.push_back(std::move(v));
+    }
+    client.participate_many(inputs, id);
+    log_info("Uploaded " + std::to_string(inputs.size()) + " participations");
     return 0;
   }
   throw SdaError("Unknown command " + cmd);

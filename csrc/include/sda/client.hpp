@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "sda/device_backend.hpp"
 #include "sda/service.hpp"
 
 namespace sda {
@@ -137,10 +138,24 @@ class SdaClient {
   void upload_encryption_key(const EncryptionKeyId& key);
   std::optional<SignedEncryptionKey> sign_export(const EncryptionKeyId& key);
 
+  // GPU execution of the roles' bulk cryptography (sda/device_backend.hpp): the
+  // clerk's open + combine + seal, the recipient's open + reconstruct + unmask and
+  // bulk participation run on the device; aggregations the device cannot take
+  // (see device_supports) use the host engines. Null = host only.
+  void set_device_backend(DeviceBackendPtr backend) { device_ = std::move(backend); }
+  DeviceBackendPtr device_backend() const { return device_; }
+  // The reason `agg` stays on the host engines, or "" when the device takes it.
+  static std::string device_unsupported(const Aggregation& agg);
+
   // Participating
   Participation new_participation(const std::vector<int64_t>& input, const AggregationId& agg);
   void upload_participation(const Participation& p);
   void participate(const std::vector<int64_t>& input, const AggregationId& agg);
+  // Many input vectors contributed by this agent, one participation each
+  // (participate.rs:37-113 per vector; keys fetched and verified once).
+  std::vector<Participation> new_participations(const std::vector<std::vector<int64_t>>& inputs,
+                                                const AggregationId& agg);
+  void participate_many(const std::vector<std::vector<int64_t>>& inputs, const AggregationId& agg);
 
   // Clerking
   bool clerk_once();
@@ -163,6 +178,7 @@ class SdaClient {
   ServicePtr service_;
   std::mutex cache_mu_;
   std::map<std::string, bool> verify_cache_;
+  DeviceBackendPtr device_;
 };
 
 }  // namespace sda

@@ -97,6 +97,13 @@ std::string base64_encode(const uint8_t* p, size_t n);
 inline std::string base64_encode(const Bytes& b) { return base64_encode(b.data(), b.size()); }
 // Strict padded decode (data-encoding `base64::decode`).
 Bytes base64_decode(const std::string& s);
+// In-place forms for bulk payloads: encode `n` bytes to `out` (room for
+// (n + 2) / 3 * 4 symbols; returns the count); the decoded length of a padded
+// string; decode into `dst` (returns the decoded length; when that exceeds
+// `cap` nothing is written). All three throw SdaError like `base64_decode`.
+size_t base64_encode_into(const uint8_t* p, size_t n, char* out);
+size_t base64_decoded_len(const char* s, size_t n);
+size_t base64_decode_into(const char* s, size_t n, uint8_t* dst, size_t cap);
 // Decode the first `encode_nopad_len(size)` characters without padding
 // (protocol/src/byte_arrays.rs:14-21: B8/B32/B64 tolerate the padding).
 Bytes base64_decode_fixed(const std::string& s, size_t size);

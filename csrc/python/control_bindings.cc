@@ -353,6 +353,33 @@ void bind_control_plane(py::module_& m) {
                              const std::string& agg) {
         c.participate(input, AggregationId::parse(agg));
       }, GilRelease())
+      .def("new_participations", [](SdaClient& c, const std::vector<std::vector<int64_t>>& inputs,
+                                    const std::string& agg) {
+        std::vector<std::string> out;
+        for (auto& p : c.new_participations(inputs, AggregationId::parse(agg))) out.push_back(enc(p));
+        return out;
+      }, GilRelease())
+      .def("participate_many", [](SdaClient& c, const std::vector<std::vector<int64_t>>& inputs,
+                                  const std::string& agg) {
+        c.participate_many(inputs, AggregationId::parse(agg));
+      }, GilRelease())
+      // GPU backend of the roles (libsda_device.so, loaded on demand)
+      .def("use_device", [](SdaClient& c, const std::string& path, int index) {
+        c.set_device_backend(load_device_backend(path, index));
+        return c.device_backend()->describe();
+      }, py::arg("path") = "", py::arg("index") = 0, GilRelease())
+      .def("use_host", [](SdaClient& c) { c.set_device_backend(nullptr); })
+      .def_property_readonly("device", [](SdaClient& c) -> std::optional<std::string> {
+        if (!c.device_backend()) return std::nullopt;
+        return c.device_backend()->describe();
+      })
+      .def("device_timings", [](SdaClient& c) {
+        return c.device_backend() ? c.device_backend()->last_timings()
+                                  : std::map<std::string, double>{};
+      })
+      .def_static("device_unsupported", [](const std::string& agg) {
+        return SdaClient::device_unsupported(dec<Aggregation>(agg));
+      })
       .def("clerk_once", &SdaClient::clerk_once, GilRelease())
       .def("run_chores", &SdaClient::run_chores, py::arg("max_iterations") = -1, GilRelease())
       .def("process_clerking_job", [](SdaClient& c, const std::string& job) {

@@ -11,6 +11,7 @@
 
 #include "sda/crypto.hpp"
 #include "sda/field.hpp"
+#include "sda/log.hpp"
 
 namespace sda {
 
@@ -383,6 +384,65 @@ Participation SdaClient::new_participation(const std::vector<int64_t>& input, co
 
 void SdaClient::upload_participation(const Participation& p) { service_->create_participation(agent_, p); }
 
+std::string SdaClient::device_unsupported(const Aggregation& agg) {
+  const auto& sh = agg.committee_sharing_scheme;
+  const auto& mk = agg.masking_scheme;
+  if (sh.modulus < 2 || sh.modulus >= ((int64_t)1 << 31)) return "the modulus does not fit 31 bits";
+  if (agg.vector_dimension == 0 || agg.vector_dimension > ((uint64_t)1 << 30)) return "vector dimension out of range";
+  if (mk.has_mask() && mk.modulus != sh.modulus) return "masking and sharing moduli differ";
+  if (mk.kind == LinearMaskingScheme::Kind::ChaCha) {
+    if (mk.seed_bitsize == 0 || mk.seed_bitsize > 256) return "ChaCha seeds of up to 256 bits";
+    if (mk.dimension != agg.vector_dimension) return "ChaCha mask dimension differs from the vector dimension";
+  }
+  if (sh.kind == LinearSecretSharingScheme::Kind::Additive) {
+    if (sh.share_count < 1 || sh.share_count > 256) return "additive sharing with 1..256 clerks";
+  } else {
+    const bool big = sh.secret_count > 8 || sh.privacy_threshold_ > 16 || sh.share_count > 64;
+    if (big && sh.modulus >= ((int64_t)1 << 28)) return "large packed-Shamir sets need a modulus below 2^28";
+    if (sh.secret_count + sh.privacy_threshold_ > 4096) return "packed-Shamir degree too large";
+  }
+  return "";
+}
+
+std::vector<Participation> SdaClient::new_participations(const std::vector<std::vector<int64_t>>& inputs,
+                                                         const AggregationId& agg_id) {
+  auto agg = service_->get_aggregation(agent_, agg_id);
+  if (!agg) throw SdaError("Could not find aggregation");
+  std::string why = device_ ? device_unsupported(*agg) : "no GPU backend";
+  if (!why.empty()) {
+    if (device_) log_warn("participate: host engines (" + why + ")");
+    std::vector<Participation> out;
+    for (auto& v : inputs) out.push_back(new_participation(v, agg_id));
+    return out;
+  }
+  for (auto& v : inputs)
+    if (v.size() != agg->vector_dimension) throw SdaError("The input length does not match the aggregation.");
+  auto committee = service_->get_committee(agent_, agg_id);
+  if (!committee) throw SdaError("Could not find committee");
+  if (committee->clerks_and_keys.size() != agg->committee_sharing_scheme.output_size())
+    throw SdaError("committee size does not match the sharing scheme");
+  std::vector<EncryptionKey> clerk_keys;
+  for (auto& ck : committee->clerks_and_keys) clerk_keys.push_back(verified_key(ck.first, ck.second, "clerk"));
+  std::optional<EncryptionKey> rk;
+  if (agg->masking_scheme.has_mask()) rk = verified_key(agg->recipient, agg->recipient_key, "recipient");
+  DeviceParticipations dp = device_->participate_many(*agg, clerk_keys, rk ? &*rk : nullptr, inputs);
+  std::vector<Participation> out(inputs.size());
+  for (size_t i = 0; i < inputs.size(); ++i) {
+    Participation& p = out[i];
+    p.id = ParticipationId::random();
+    p.participant = agent_.id;
+    p.aggregation = agg->id;
+    if (rk) p.recipient_encryption = std::move(dp.mask_boxes[i]);
+    for (size_t c = 0; c < clerk_keys.size(); ++c)
+      p.clerk_encryptions.emplace_back(committee->clerks_and_keys[c].first, std::move(dp.clerk_boxes[i][c]));
+  }
+  return out;
+}
+
+void SdaClient::participate_many(const std::vector<std::vector<int64_t>>& inputs, const AggregationId& agg) {
+  for (auto& p : new_participations(inputs, agg)) upload_participation(p);
+}
+
 void SdaClient::participate(const std::vector<int64_t>& input, const AggregationId& agg) {
   upload_participation(new_participation(input, agg));
 }
@@ -416,6 +476,19 @@ ClerkingResult SdaClient::process_clerking_job(const ClerkingJob& job) {
   if (!own) throw SdaError("Could not find own encryption key in keyset");
   auto kp = keystore_->get<EncryptionKeypair>(own->str());
   if (!kp) throw SdaError("Could not load keypair for decryption");
+  if (device_) {
+    std::string why = device_unsupported(*agg);
+    if (why.empty()) {
+      const auto& sh = agg->committee_sharing_scheme;
+      const size_t values = (agg->vector_dimension + sh.input_size() - 1) / sh.input_size();
+      std::vector<BoxSource> boxes;
+      boxes.reserve(job.encryptions.size());
+      for (auto& e : job.encryptions) boxes.push_back(box_source(e));
+      EncryptionKey ek = verified_key(agg->recipient, agg->recipient_key, "recipient");
+      return ClerkingResult{job.id, job.clerk, device_->clerk_combine(sh, values, *kp, boxes, ek)};
+    }
+    log_warn("clerk: host engines (" + why + ")");
+  }
   std::vector<std::vector<int64_t>> parts;
   parts.reserve(job.encryptions.size());
   for (auto& e : job.encryptions) parts.push_back(decrypt_shares(*kp, e));
@@ -462,6 +535,24 @@ RecipientOutput SdaClient::reveal_aggregation(const AggregationId& id) {
   if (!result) throw SdaError("Missing aggregation result");
   auto kp = keystore_->get<EncryptionKeypair>(agg->recipient_key.str());
   if (!kp) throw SdaError("Could not load keypair for decryption");
+  if (device_) {
+    std::string why = device_unsupported(*agg);
+    if (why.empty()) {
+      std::vector<std::pair<size_t, BoxSource>> results;
+      for (auto& cr_ : result->clerk_encryptions) {
+        size_t idx = committee->clerks_and_keys.size();
+        for (size_t i = 0; i < committee->clerks_and_keys.size(); ++i)
+          if (committee->clerks_and_keys[i].first == cr_.clerk) { idx = i; break; }
+        if (idx == committee->clerks_and_keys.size()) throw SdaError("Missing clerk, " + cr_.clerk.str());
+        results.emplace_back(idx, box_source(cr_.encryption));
+      }
+      std::vector<BoxSource> masks;
+      if (result->recipient_encryptions)
+        for (auto& e : *result->recipient_encryptions) masks.push_back(box_source(e));
+      return RecipientOutput{agg->modulus, device_->reveal(*agg, *kp, results, masks)};
+    }
+    log_warn("reveal: host engines (" + why + ")");
+  }
   std::vector<int64_t> mask;
   if (result->recipient_encryptions) {
     std::vector<std::vector<int64_t>> masks;

@@ -365,62 +365,108 @@ Value Value::parse(const std::string& text) {
 }  // namespace json
 
 // ---- base64 ------------------------------------------------------------------
+// Table-driven, four symbols (three bytes) per step: sealed boxes of megabytes
+// cross the REST API as base64 strings, so this codec is on the data path of
+// every role.
 static const char* kB64 = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
 
-std::string base64_encode(const uint8_t* p, size_t n) {
-  std::string out;
-  out.reserve((n + 2) / 3 * 4);
+namespace {
+struct B64Tables {
+  uint8_t val[256];  // 0..63, or 0xff for a symbol outside the alphabet
+  B64Tables() {
+    std::memset(val, 0xff, sizeof(val));
+    for (int i = 0; i < 64; ++i) val[(uint8_t)kB64[i]] = (uint8_t)i;
+  }
+};
+const B64Tables& b64_tables() {
+  static const B64Tables t;
+  return t;
+}
+}  // namespace
+
+size_t base64_encode_into(const uint8_t* p, size_t n, char* out) {
+  char* o = out;
   size_t i = 0;
   for (; i + 3 <= n; i += 3) {
-    uint32_t v = (p[i] << 16) | (p[i + 1] << 8) | p[i + 2];
-    out.push_back(kB64[v >> 18]);
-    out.push_back(kB64[(v >> 12) & 63]);
-    out.push_back(kB64[(v >> 6) & 63]);
-    out.push_back(kB64[v & 63]);
+    uint32_t v = ((uint32_t)p[i] << 16) | ((uint32_t)p[i + 1] << 8) | p[i + 2];
+    o[0] = kB64[v >> 18];
+    o[1] = kB64[(v >> 12) & 63];
+    o[2] = kB64[(v >> 6) & 63];
+    o[3] = kB64[v & 63];
+    o += 4;
   }
   if (n - i == 1) {
-    uint32_t v = p[i] << 16;
-    out.push_back(kB64[v >> 18]);
-    out.push_back(kB64[(v >> 12) & 63]);
-    out += "==";
+    uint32_t v = (uint32_t)p[i] << 16;
+    o[0] = kB64[v >> 18];
+    o[1] = kB64[(v >> 12) & 63];
+    o[2] = o[3] = '=';
+    o += 4;
   } else if (n - i == 2) {
-    uint32_t v = (p[i] << 16) | (p[i + 1] << 8);
-    out.push_back(kB64[v >> 18]);
-    out.push_back(kB64[(v >> 12) & 63]);
-    out.push_back(kB64[(v >> 6) & 63]);
-    out.push_back('=');
+    uint32_t v = ((uint32_t)p[i] << 16) | ((uint32_t)p[i + 1] << 8);
+    o[0] = kB64[v >> 18];
+    o[1] = kB64[(v >> 12) & 63];
+    o[2] = kB64[(v >> 6) & 63];
+    o[3] = '=';
+    o += 4;
   }
+  return (size_t)(o - out);
+}
+
+std::string base64_encode(const uint8_t* p, size_t n) {
+  std::string out((n + 2) / 3 * 4, '\0');
+  base64_encode_into(p, n, &out[0]);
   return out;
 }
 
-static int b64val(char c) {
-  if (c >= 'A' && c <= 'Z') return c - 'A';
-  if (c >= 'a' && c <= 'z') return c - 'a' + 26;
-  if (c >= '0' && c <= '9') return c - '0' + 52;
-  if (c == '+') return 62;
-  if (c == '/') return 63;
-  return -1;
+// Unpadded decode of `len` symbols into `dst` (room for len * 3 / 4 bytes).
+static size_t decode_nopad_into(const char* s, size_t len, uint8_t* dst) {
+  const uint8_t* T = b64_tables().val;
+  if (len % 4 == 1) throw SdaError("Base64 decoding error: invalid length");
+  uint8_t* o = dst;
+  size_t i = 0;
+  uint32_t bad = 0;
+  for (; i + 4 <= len; i += 4) {
+    uint32_t a = T[(uint8_t)s[i]], b = T[(uint8_t)s[i + 1]], c = T[(uint8_t)s[i + 2]],
+             d = T[(uint8_t)s[i + 3]];
+    bad |= a | b | c | d;  // 0xff marks a foreign symbol: bit 7 survives the OR
+    uint32_t v = (a << 18) | (b << 12) | (c << 6) | d;
+    o[0] = (uint8_t)(v >> 16);
+    o[1] = (uint8_t)(v >> 8);
+    o[2] = (uint8_t)v;
+    o += 3;
+  }
+  if (bad & 0x80) throw SdaError("Base64 decoding error: invalid symbol");
+  size_t rest = len - i;
+  if (rest) {  // 2 or 3 symbols: 1 or 2 bytes, trailing bits must be zero
+    uint32_t a = T[(uint8_t)s[i]], b = T[(uint8_t)s[i + 1]], c = rest == 3 ? T[(uint8_t)s[i + 2]] : 0;
+    if ((a | b | c) & 0x80) throw SdaError("Base64 decoding error: invalid symbol");
+    uint32_t v = (a << 18) | (b << 12) | (c << 6);
+    *o++ = (uint8_t)(v >> 16);
+    if (rest == 3) *o++ = (uint8_t)(v >> 8);
+    if (v & (rest == 3 ? 0xffu : 0xffffu))
+      throw SdaError("Base64 decoding error: non-zero trailing bits");
+  }
+  return (size_t)(o - dst);
+}
+
+size_t base64_decoded_len(const char* s, size_t n) {
+  if (n % 4 != 0) throw SdaError("Base64 decoding error: invalid length");
+  size_t pad = 0;
+  while (pad < 2 && n > pad && s[n - 1 - pad] == '=') ++pad;
+  return n / 4 * 3 - pad;
+}
+
+size_t base64_decode_into(const char* s, size_t n, uint8_t* dst, size_t cap) {
+  size_t want = base64_decoded_len(s, n);
+  if (want > cap) return want;  // does not fit: nothing written
+  size_t len = n;
+  while (len > 0 && n - len < 2 && s[len - 1] == '=') --len;
+  return decode_nopad_into(s, len, dst);
 }
 
 static Bytes decode_nopad(const std::string& s, size_t len) {
-  Bytes out;
-  out.reserve(len * 3 / 4);
-  uint32_t acc = 0;
-  int bits = 0;
-  for (size_t i = 0; i < len; ++i) {
-    int v = b64val(s[i]);
-    if (v < 0) throw SdaError("Base64 decoding error: invalid symbol");
-    acc = (acc << 6) | (uint32_t)v;
-    bits += 6;
-    if (bits >= 8) {
-      bits -= 8;
-      out.push_back((uint8_t)(acc >> bits));
-    }
-  }
-  // trailing bits must be zero (canonical encoding)
-  if (bits > 0 && (acc & ((1u << bits) - 1)) != 0)
-    throw SdaError("Base64 decoding error: non-zero trailing bits");
-  if (len % 4 == 1) throw SdaError("Base64 decoding error: invalid length");
+  Bytes out(len * 3 / 4 + 3);
+  out.resize(decode_nopad_into(s.data(), len, out.data()));
   return out;
 }
 

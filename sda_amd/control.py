@@ -309,17 +309,40 @@ def http_handle(server: ServerService, method: str, target: str,
 class SdaClient:
     """Agent roles over any ``Service`` (client/src/lib.rs:28-47)."""
 
-    def __init__(self, agent: Obj, keystore, service: Service):
+    def __init__(self, agent: Obj, keystore, service: Service, device: Optional[str] = None):
+        """`device`: None / "cpu" = the host engines; "gpu" or "gpu:N" = the roles'
+        bulk cryptography (clerk jobs, reveal, bulk participation) on MI355X N
+        through ``libsda_device.so`` (raises if the library or a GPU is missing)."""
         self.service = service
         self.keystore = keystore
         self._h = _c().Client(_enc(agent), keystore, service.handle)
+        if device not in (None, "", "cpu", "host"):
+            self.use_device(device)
+
+    def use_device(self, device: str = "gpu", library: str = "") -> str:
+        """Switch the roles to the GPU backend; returns its description."""
+        kind, _, index = device.partition(":")
+        if kind != "gpu":
+            raise ValueError("device must be 'cpu', 'gpu' or 'gpu:N'")
+        return self._h.use_device(library, int(index or 0))
+
+    def use_host(self) -> None:
+        self._h.use_host()
+
+    @property
+    def device(self) -> Optional[str]:
+        return self._h.device
+
+    def device_timings(self) -> Dict[str, float]:
+        """Milliseconds of the last GPU role call's stages."""
+        return dict(self._h.device_timings())
 
     @classmethod
     def create(cls, keystore, service: Service, upload: bool = True,
-               encryption_key: bool = True) -> "SdaClient":
+               encryption_key: bool = True, device: Optional[str] = None) -> "SdaClient":
         """new_agent + (optionally) upload_agent + new/upload encryption key."""
         agent = json.loads(_c().Client.new_agent(keystore))
-        cl = cls(agent, keystore, service)
+        cl = cls(agent, keystore, service, device=device)
         if upload:
             cl.upload_agent()
             if encryption_key:
@@ -356,6 +379,15 @@ class SdaClient:
 
     def participate(self, values: Sequence[int], aggregation_id: str) -> None:
         self._h.participate(list(values), aggregation_id)
+
+    def new_participations(self, vectors: Sequence[Sequence[int]], aggregation_id: str) -> List[Obj]:
+        """One participation per input vector, sealed in bulk (on the GPU backend
+        when one is set)."""
+        return [json.loads(t) for t in
+                self._h.new_participations([list(v) for v in vectors], aggregation_id)]
+
+    def participate_many(self, vectors: Sequence[Sequence[int]], aggregation_id: str) -> None:
+        self._h.participate_many([list(v) for v in vectors], aggregation_id)
 
     # clerking
     def clerk_once(self) -> bool:
