@@ -161,12 +161,20 @@ class SdaClient {
   bool clerk_once();
   void run_chores(long max_iterations);
   ClerkingResult process_clerking_job(const ClerkingJob& job);
+  // The same over box sources (`job.encryptions` is not read): the boxes may
+  // still be base64 text inside the job's JSON.
+  ClerkingResult process_clerking_boxes(const ClerkingJob& job, const std::vector<BoxSource>& boxes);
 
   // Receiving
   void upload_aggregation(const Aggregation& a);
   void begin_aggregation(const AggregationId& a);
   void end_aggregation(const AggregationId& a);
   RecipientOutput reveal_aggregation(const AggregationId& a);
+
+  // Wall-clock milliseconds of the last clerk_once / reveal_aggregation:
+  // "fetch" (service calls: HTTP, JSON, base64), "process" (the cryptography),
+  // "post" (result upload).
+  std::map<std::string, double> role_timings() const { return role_timings_; }
 
   // signing.rs:107-131, with the result cached per (agent, key) (reference FIXME)
   bool signature_is_valid(const Agent& signer, const SignedEncryptionKey& key);
@@ -179,6 +187,7 @@ class SdaClient {
   std::mutex cache_mu_;
   std::map<std::string, bool> verify_cache_;
   DeviceBackendPtr device_;
+  std::map<std::string, double> role_timings_;
 };
 
 }  // namespace sda

@@ -116,6 +116,10 @@ class SdaHttpClient : public SdaService {
   void create_snapshot(const Agent& caller, const Snapshot& s) override;
   std::optional<SnapshotResult> get_snapshot_result(const Agent& caller, const AggregationId& a,
                                                     const SnapshotId& s) override;
+  // the bulk downloads as received (no JSON tree is built)
+  std::optional<std::string> get_clerking_job_json(const Agent& caller, const AgentId& clerk) override;
+  std::optional<std::string> get_snapshot_result_json(const Agent& caller, const AggregationId& a,
+                                                      const SnapshotId& s) override;
 
   struct Reply {
     int status = 0;
@@ -128,6 +132,8 @@ class SdaHttpClient : public SdaService {
  private:
   // process(): status -> Some(json) / None / typed error (client-http/src/client.rs:43-102)
   std::optional<json::Value> call(const std::string& method, const std::string& path,
+                                  const Agent* caller, const std::string* body);
+  std::optional<std::string> call_text(const std::string& method, const std::string& path,
                                   const Agent* caller, const std::string* body);
   std::string host_;
   int port_ = 80;

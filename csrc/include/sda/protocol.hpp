@@ -346,6 +346,31 @@ std::string encode(const T& x) { return to_json(x).dump(); }
 template <class T>
 T decode(const std::string& s) { return from_json<T>(Value::parse(s)); }
 
+// Zero-copy views of the bulk downloads (wire_views.cc): where each base64
+// payload sits inside the response text. nullopt = the text is not in the plain
+// shape serde_json emits; use decode<>() instead.
+struct TextSpan {
+  size_t off = 0, len = 0;
+};
+struct ClerkingJobView {
+  ClerkingJob head;             // `encryptions` left empty
+  std::vector<TextSpan> boxes;  // base64 of encryptions[i]
+};
+struct SnapshotResultView {
+  struct Result {
+    ClerkingJobId job;
+    AgentId clerk;
+    TextSpan box;
+  };
+  SnapshotId snapshot;
+  uint64_t number_of_participations = 0;
+  std::vector<Result> results;
+  bool has_masks = false;
+  std::vector<TextSpan> masks;
+};
+std::optional<ClerkingJobView> scan_clerking_job(const std::string& text);
+std::optional<SnapshotResultView> scan_snapshot_result(const std::string& text);
+
 // Canonical bytes for signing (helpers.rs:130-142): compact JSON.
 template <class T>
 Bytes canonical(const T& x) {

@@ -35,8 +35,12 @@ class SdaServer {
   void create_snapshot(const Snapshot& s);  // snapshot.rs:4-47
   std::optional<ClerkingJob> poll_clerking_job(const AgentId& clerk);
   std::optional<ClerkingJob> get_clerking_job(const AgentId& clerk, const ClerkingJobId& job);
+  // bulk forms (see ClerkingJobsStore): the job as stored text, its head only
+  std::optional<std::string> poll_clerking_job_json(const AgentId& clerk);
+  std::optional<ClerkingJob> get_clerking_job_head(const AgentId& clerk, const ClerkingJobId& job);
   void create_clerking_result(const ClerkingResult& r);
   std::optional<SnapshotResult> get_snapshot_result(const AggregationId& a, const SnapshotId& s);
+  std::optional<std::string> get_snapshot_result_json(const AggregationId& a, const SnapshotId& s);
   // auth (server.rs:171-190)
   void upsert_auth_token(const AuthToken& token);
   Agent check_auth_token(const AuthToken& token);  // throws InvalidCredentials
@@ -72,6 +76,9 @@ class SdaServerService : public SdaService {
   std::optional<Committee> get_committee(const Agent& caller, const AggregationId& a) override;
   void create_participation(const Agent& caller, const Participation& p) override;
   std::optional<ClerkingJob> get_clerking_job(const Agent& caller, const AgentId& clerk) override;
+  std::optional<std::string> get_clerking_job_json(const Agent& caller, const AgentId& clerk) override;
+  std::optional<std::string> get_snapshot_result_json(const Agent& caller, const AggregationId& a,
+                                                      const SnapshotId& s) override;
   void create_clerking_result(const Agent& caller, const ClerkingResult& r) override;
   void create_aggregation(const Agent& caller, const Aggregation& a) override;
   void delete_aggregation(const Agent& caller, const AggregationId& a) override;

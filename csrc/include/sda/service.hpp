@@ -55,6 +55,25 @@ class SdaService {
   virtual std::optional<SnapshotResult> get_snapshot_result(const Agent& caller,
                                                             const AggregationId& aggregation,
                                                             const SnapshotId& snapshot) = 0;
+
+  // The two bulk downloads as the JSON text of their responses (a clerking job
+  // holds a sealed box per participation, a snapshot result a mask box per
+  // participation). Implementations that hold or receive the text anyway (the
+  // server's stores, the REST client) return it without building the structs;
+  // `wire::scan_*` then locates the payloads in place. Defaults encode the
+  // struct forms.
+  virtual std::optional<std::string> get_clerking_job_json(const Agent& caller, const AgentId& clerk) {
+    auto j = get_clerking_job(caller, clerk);
+    if (!j) return std::nullopt;
+    return wire::encode(*j);
+  }
+  virtual std::optional<std::string> get_snapshot_result_json(const Agent& caller,
+                                                              const AggregationId& aggregation,
+                                                              const SnapshotId& snapshot) {
+    auto r = get_snapshot_result(caller, aggregation, snapshot);
+    if (!r) return std::nullopt;
+    return wire::encode(*r);
+  }
 };
 
 using ServicePtr = std::shared_ptr<SdaService>;

@@ -75,6 +75,9 @@ class AggregationsStore {
       const AggregationId& aggregation, const SnapshotId& snapshot, size_t clerks);
   virtual void create_snapshot_mask(const SnapshotId& snapshot, const std::vector<Encryption>& mask) = 0;
   virtual std::optional<std::vector<Encryption>> get_snapshot_mask(const SnapshotId& snapshot) = 0;
+  // The mask boxes as the JSON text of the array (stores that hold text return
+  // it as stored; the default encodes get_snapshot_mask()).
+  virtual std::optional<std::string> get_snapshot_mask_json(const SnapshotId& snapshot);
 };
 
 class ClerkingJobsStore {
@@ -89,6 +92,15 @@ class ClerkingJobsStore {
   virtual std::vector<ClerkingJobId> list_results(const SnapshotId& snapshot) = 0;
   virtual std::optional<ClerkingResult> get_result(const SnapshotId& snapshot,
                                                    const ClerkingJobId& job) = 0;
+  // Bulk forms. A job holds a sealed box per participation: serving it as the
+  // text the store holds, and reading only its head for the result ACL, keeps
+  // the server from decoding and re-encoding hundreds of megabytes per request.
+  // Defaults go through the struct forms.
+  virtual std::optional<std::string> poll_clerking_job_json(const AgentId& clerk);
+  virtual std::optional<ClerkingJob> get_clerking_job_head(const AgentId& clerk,
+                                                           const ClerkingJobId& job);  // may lack the boxes
+  virtual std::optional<std::string> get_result_json(const SnapshotId& snapshot,
+                                                     const ClerkingJobId& job);
 };
 
 struct Stores {

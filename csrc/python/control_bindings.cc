@@ -9,6 +9,7 @@
 // server/src/lib.rs:34-45 (memory/JFS factories), server-store-mongodb
 // (document store), server-http/src/lib.rs (REST server), client-http
 // (REST client), client/src/lib.rs (SdaClient roles), client-store (stores).
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -189,6 +190,16 @@ void bind_control_plane(py::module_& m) {
                                      const std::string& agg, const std::string& snap) {
         return enc_opt(s.get_snapshot_result(dec<Agent>(caller), AggregationId::parse(agg),
                                              SnapshotId::parse(snap)));
+      }, GilRelease())
+      // the bulk downloads as the response text (see SdaService)
+      .def("get_clerking_job_json", [](SdaService& s, const std::string& caller,
+                                       const std::string& clerk) {
+        return s.get_clerking_job_json(dec<Agent>(caller), AgentId::parse(clerk));
+      }, GilRelease())
+      .def("get_snapshot_result_json", [](SdaService& s, const std::string& caller,
+                                          const std::string& agg, const std::string& snap) {
+        return s.get_snapshot_result_json(dec<Agent>(caller), AggregationId::parse(agg),
+                                          SnapshotId::parse(snap));
       }, GilRelease());
 
   // in-process server: the service plus server-side helpers (auth tokens)
@@ -325,6 +336,24 @@ void bind_control_plane(py::module_& m) {
     return decrypt_shares(dec<EncryptionKeypair>(kp), dec<Encryption>(e));
   }, GilRelease());
 
+  // ---- zero-copy views of the bulk downloads (wire_views.cc) --------------------
+  c.def("scan_clerking_job", [](const std::string& text) -> py::object {
+    auto v = wire::scan_clerking_job(text);
+    if (!v) return py::none();
+    std::vector<std::pair<size_t, size_t>> spans;
+    for (auto& s : v->boxes) spans.emplace_back(s.off, s.len);
+    return py::make_tuple(enc(v->head), spans);
+  });
+  c.def("scan_snapshot_result", [](const std::string& text) -> py::object {
+    auto v = wire::scan_snapshot_result(text);
+    if (!v) return py::none();
+    std::vector<std::tuple<std::string, std::string, size_t, size_t>> results;
+    for (auto& r : v->results) results.emplace_back(r.job.str(), r.clerk.str(), r.box.off, r.box.len);
+    std::vector<std::pair<size_t, size_t>> masks;
+    for (auto& s : v->masks) masks.emplace_back(s.off, s.len);
+    return py::make_tuple(v->snapshot.str(), v->number_of_participations, results, v->has_masks, masks);
+  });
+
   // ---- client roles (client/src/lib.rs + participate/clerk/receive/maintenance)
   py::class_<SdaClient, std::shared_ptr<SdaClient>>(c, "Client")
       .def(py::init([](const std::string& agent, StorePtr ks, ServicePtr svc) {
@@ -376,6 +405,16 @@ void bind_control_plane(py::module_& m) {
       .def("device_timings", [](SdaClient& c) {
         return c.device_backend() ? c.device_backend()->last_timings()
                                   : std::map<std::string, double>{};
+      })
+      .def("role_timings", &SdaClient::role_timings)
+      .def("participate_array", [](SdaClient& c, py::array_t<int64_t, py::array::c_style | py::array::forcecast> a,
+                                   const std::string& agg) {
+        if (a.ndim() != 2) throw std::invalid_argument("participate_array: expected a [P][D] array");
+        std::vector<std::vector<int64_t>> inputs(a.shape(0));
+        const int64_t* p = a.data();
+        for (ssize_t i = 0; i < a.shape(0); ++i) inputs[i].assign(p + i * a.shape(1), p + (i + 1) * a.shape(1));
+        py::gil_scoped_release nogil;
+        c.participate_many(inputs, AggregationId::parse(agg));
       })
       .def_static("device_unsupported", [](const std::string& agg) {
         return SdaClient::device_unsupported(dec<Aggregation>(agg));

@@ -4,10 +4,12 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cerrno>
 #include <cstdio>
 #include <fstream>
 #include <sstream>
+#include <thread>
 
 #include "sda/crypto.hpp"
 #include "sda/field.hpp"
@@ -371,11 +373,29 @@ Participation SdaClient::new_participation(const std::vector<int64_t>& input, co
   auto shares = generate_shares(agg->committee_sharing_scheme, mr.masked_secrets);
   if (shares.size() != committee->clerks_and_keys.size())
     throw SdaError("committee size does not match the sharing scheme");
+  // participate.rs:82-101: one sealed box per clerk. Keys are fetched and verified
+  // in order; the n seals are independent and run side by side.
+  std::vector<EncryptionKey> eks;
   for (size_t i = 0; i < shares.size(); ++i) {
     const auto& ck = committee->clerks_and_keys[i];
-    EncryptionKey ek = verified_key(ck.first, ck.second, "clerk");
-    p.clerk_encryptions.emplace_back(ck.first, encrypt_shares(ek, shares[i]));
+    eks.push_back(verified_key(ck.first, ck.second, "clerk"));
   }
+  std::vector<Encryption> sealed(shares.size());
+  const bool threaded = shares.size() > 1 && !shares[0].empty() && shares[0].size() * shares.size() >= 4096;
+  if (threaded) {
+    std::vector<std::thread> workers;
+    const size_t nthreads = std::min<size_t>({shares.size(), (size_t)8,
+                                              (size_t)std::max(1u, std::thread::hardware_concurrency())});
+    for (size_t tid = 0; tid < nthreads; ++tid)
+      workers.emplace_back([&, tid] {
+        for (size_t i = tid; i < shares.size(); i += nthreads) sealed[i] = encrypt_shares(eks[i], shares[i]);
+      });
+    for (auto& w : workers) w.join();
+  } else {
+    for (size_t i = 0; i < shares.size(); ++i) sealed[i] = encrypt_shares(eks[i], shares[i]);
+  }
+  for (size_t i = 0; i < shares.size(); ++i)
+    p.clerk_encryptions.emplace_back(committee->clerks_and_keys[i].first, std::move(sealed[i]));
   p.id = ParticipationId::random();
   p.participant = agent_.id;
   p.aggregation = agg->id;
@@ -447,11 +467,36 @@ void SdaClient::participate(const std::vector<int64_t>& input, const Aggregation
   upload_participation(new_participation(input, agg));
 }
 
+namespace {
+double ms_since(std::chrono::steady_clock::time_point& t0) {
+  auto t1 = std::chrono::steady_clock::now();
+  double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  t0 = t1;
+  return ms;
+}
+}  // namespace
+
 bool SdaClient::clerk_once() {
-  auto job = service_->get_clerking_job(agent_, agent_.id);
-  if (!job) return false;
-  ClerkingResult r = process_clerking_job(*job);
+  auto t = std::chrono::steady_clock::now();
+  // the job as JSON text: its boxes are decoded from where they sit in the text
+  auto text = service_->get_clerking_job_json(agent_, agent_.id);
+  if (!text) return false;
+  role_timings_.clear();
+  ClerkingResult r;
+  if (auto view = wire::scan_clerking_job(*text)) {
+    role_timings_["fetch"] = ms_since(t);
+    std::vector<BoxSource> boxes;
+    boxes.reserve(view->boxes.size());
+    for (auto& sp : view->boxes) boxes.push_back(box_source_base64(text->data() + sp.off, sp.len));
+    r = process_clerking_boxes(view->head, boxes);
+  } else {
+    ClerkingJob job = wire::decode<ClerkingJob>(*text);
+    role_timings_["fetch"] = ms_since(t);
+    r = process_clerking_job(job);
+  }
+  role_timings_["process"] = ms_since(t);
   service_->create_clerking_result(agent_, r);
+  role_timings_["post"] = ms_since(t);
   return true;
 }
 
@@ -466,6 +511,25 @@ void SdaClient::run_chores(long max_iterations) {
 }
 
 ClerkingResult SdaClient::process_clerking_job(const ClerkingJob& job) {
+  std::vector<BoxSource> boxes;
+  boxes.reserve(job.encryptions.size());
+  for (auto& e : job.encryptions) boxes.push_back(box_source(e));
+  return process_clerking_boxes(job, boxes);
+}
+
+namespace {
+// A box materialised from its source (the host engines take owned bytes).
+Encryption materialise(const BoxSource& src) {
+  Encryption e;
+  e.sodium.resize(src.max_len);
+  size_t n = src.fill(e.sodium.data(), e.sodium.size());
+  if (n > e.sodium.size()) throw SdaError("Sodium decryption failure: box longer than announced");
+  e.sodium.resize(n);
+  return e;
+}
+}  // namespace
+
+ClerkingResult SdaClient::process_clerking_boxes(const ClerkingJob& job, const std::vector<BoxSource>& boxes) {
   auto agg = service_->get_aggregation(agent_, job.aggregation);
   if (!agg) throw SdaError("Unknown aggregation");
   auto committee = service_->get_committee(agent_, job.aggregation);
@@ -481,18 +545,48 @@ ClerkingResult SdaClient::process_clerking_job(const ClerkingJob& job) {
     if (why.empty()) {
       const auto& sh = agg->committee_sharing_scheme;
       const size_t values = (agg->vector_dimension + sh.input_size() - 1) / sh.input_size();
-      std::vector<BoxSource> boxes;
-      boxes.reserve(job.encryptions.size());
-      for (auto& e : job.encryptions) boxes.push_back(box_source(e));
       EncryptionKey ek = verified_key(agg->recipient, agg->recipient_key, "recipient");
       return ClerkingResult{job.id, job.clerk, device_->clerk_combine(sh, values, *kp, boxes, ek)};
     }
     log_warn("clerk: host engines (" + why + ")");
   }
-  std::vector<std::vector<int64_t>> parts;
-  parts.reserve(job.encryptions.size());
-  for (auto& e : job.encryptions) parts.push_back(decrypt_shares(*kp, e));
-  auto combined = combine_shares(agg->committee_sharing_scheme, parts);
+  // clerk.rs:79-86: open every box and fold it into a running sum. The boxes are
+  // independent, so a few threads each fold a share of them (the reference's
+  // `(a + b) % m` per element; partial sums are folded the same way).
+  const int64_t m = agg->committee_sharing_scheme.modulus;
+  const size_t nthreads = std::max<size_t>(1, std::min<size_t>({boxes.size() / 4, (size_t)8,
+                                          (size_t)std::max(1u, std::thread::hardware_concurrency())}));
+  std::vector<std::vector<int64_t>> partial(nthreads);
+  std::vector<std::string> failure(nthreads);
+  auto fold = [&](size_t tid) {
+    try {
+      std::vector<int64_t>& acc = partial[tid];
+      bool first = true;
+      for (size_t j = tid; j < boxes.size(); j += nthreads) {
+        std::vector<int64_t> part = decrypt_shares(*kp, materialise(boxes[j]));
+        if (first) {
+          acc.assign(part.size(), 0);
+          first = false;
+        }
+        if (part.size() != acc.size()) throw SdaError("Wrong dimension");
+        for (size_t i = 0; i < part.size(); ++i) acc[i] = (acc[i] + part[i]) % m;
+      }
+    } catch (const std::exception& e) {
+      failure[tid] = e.what();
+      if (failure[tid].empty()) failure[tid] = "clerking failed";
+    }
+  };
+  std::vector<std::thread> workers;
+  for (size_t tid = 1; tid < nthreads; ++tid) workers.emplace_back(fold, tid);
+  fold(0);
+  for (auto& w : workers) w.join();
+  for (auto& f : failure)
+    if (!f.empty()) throw SdaError(f);
+  std::vector<int64_t> combined = boxes.empty() ? std::vector<int64_t>{} : partial[0];
+  for (size_t tid = 1; tid < nthreads; ++tid) {
+    if (partial[tid].size() != combined.size()) throw SdaError("Wrong dimension");
+    for (size_t i = 0; i < combined.size(); ++i) combined[i] = (combined[i] + partial[tid][i]) % m;
+  }
   EncryptionKey ek = verified_key(agg->recipient, agg->recipient_key, "recipient");
   return ClerkingResult{job.id, job.clerk, encrypt_shares(ek, combined)};
 }
@@ -521,6 +615,13 @@ void SdaClient::end_aggregation(const AggregationId& id) {
 }
 
 RecipientOutput SdaClient::reveal_aggregation(const AggregationId& id) {
+  auto t = std::chrono::steady_clock::now();
+  struct Stamp {  // "process" = everything after the fetch, however the function returns
+    SdaClient& c;
+    std::chrono::steady_clock::time_point& t;
+    ~Stamp() { c.role_timings_["process"] = ms_since(t); }
+  } stamp{*this, t};
+  role_timings_.clear();
   auto agg = service_->get_aggregation(agent_, id);
   if (!agg) throw SdaError("Unknown aggregation, " + id.str());
   auto committee = service_->get_committee(agent_, id);
@@ -531,42 +632,50 @@ RecipientOutput SdaClient::reveal_aggregation(const AggregationId& id) {
   for (auto& s : status->snapshots)
     if (s.result_ready) { snap = &s; break; }
   if (!snap) throw SdaError("Aggregation not ready");
-  auto result = service_->get_snapshot_result(agent_, id, snap->id);
-  if (!result) throw SdaError("Missing aggregation result");
+  // the result as JSON text: the boxes are decoded from where they sit in it
+  auto text = service_->get_snapshot_result_json(agent_, id, snap->id);
+  if (!text) throw SdaError("Missing aggregation result");
+  std::vector<std::pair<AgentId, BoxSource>> by_clerk;
+  std::vector<BoxSource> masks;
+  bool has_masks = false;
+  std::optional<SnapshotResult> owned;  // backs the sources when the text is not in the plain shape
+  if (auto view = wire::scan_snapshot_result(*text)) {
+    for (auto& r : view->results)
+      by_clerk.emplace_back(r.clerk, box_source_base64(text->data() + r.box.off, r.box.len));
+    has_masks = view->has_masks;
+    for (auto& sp : view->masks) masks.push_back(box_source_base64(text->data() + sp.off, sp.len));
+  } else {
+    owned = wire::decode<SnapshotResult>(*text);
+    for (auto& cr_ : owned->clerk_encryptions) by_clerk.emplace_back(cr_.clerk, box_source(cr_.encryption));
+    has_masks = owned->recipient_encryptions.has_value();
+    if (has_masks)
+      for (auto& e : *owned->recipient_encryptions) masks.push_back(box_source(e));
+  }
+  role_timings_["fetch"] = ms_since(t);
   auto kp = keystore_->get<EncryptionKeypair>(agg->recipient_key.str());
   if (!kp) throw SdaError("Could not load keypair for decryption");
+  // receive.rs:127-138: each result's clerk -> its committee index
+  std::vector<std::pair<size_t, BoxSource>> results;
+  for (auto& cb : by_clerk) {
+    size_t idx = committee->clerks_and_keys.size();
+    for (size_t i = 0; i < committee->clerks_and_keys.size(); ++i)
+      if (committee->clerks_and_keys[i].first == cb.first) { idx = i; break; }
+    if (idx == committee->clerks_and_keys.size()) throw SdaError("Missing clerk, " + cb.first.str());
+    results.emplace_back(idx, cb.second);
+  }
   if (device_) {
     std::string why = device_unsupported(*agg);
-    if (why.empty()) {
-      std::vector<std::pair<size_t, BoxSource>> results;
-      for (auto& cr_ : result->clerk_encryptions) {
-        size_t idx = committee->clerks_and_keys.size();
-        for (size_t i = 0; i < committee->clerks_and_keys.size(); ++i)
-          if (committee->clerks_and_keys[i].first == cr_.clerk) { idx = i; break; }
-        if (idx == committee->clerks_and_keys.size()) throw SdaError("Missing clerk, " + cr_.clerk.str());
-        results.emplace_back(idx, box_source(cr_.encryption));
-      }
-      std::vector<BoxSource> masks;
-      if (result->recipient_encryptions)
-        for (auto& e : *result->recipient_encryptions) masks.push_back(box_source(e));
-      return RecipientOutput{agg->modulus, device_->reveal(*agg, *kp, results, masks)};
-    }
+    if (why.empty()) return RecipientOutput{agg->modulus, device_->reveal(*agg, *kp, results, masks)};
     log_warn("reveal: host engines (" + why + ")");
   }
   std::vector<int64_t> mask;
-  if (result->recipient_encryptions) {
-    std::vector<std::vector<int64_t>> masks;
-    for (auto& e : *result->recipient_encryptions) masks.push_back(decrypt_shares(*kp, e));
-    mask = combine_masks(agg->masking_scheme, masks);
+  if (has_masks) {
+    std::vector<std::vector<int64_t>> opened;
+    for (auto& src : masks) opened.push_back(decrypt_shares(*kp, materialise(src)));
+    mask = combine_masks(agg->masking_scheme, opened);
   }
   std::vector<std::pair<size_t, std::vector<int64_t>>> indexed;
-  for (auto& cr_ : result->clerk_encryptions) {
-    size_t idx = committee->clerks_and_keys.size();
-    for (size_t i = 0; i < committee->clerks_and_keys.size(); ++i)
-      if (committee->clerks_and_keys[i].first == cr_.clerk) { idx = i; break; }
-    if (idx == committee->clerks_and_keys.size()) throw SdaError("Missing clerk, " + cr_.clerk.str());
-    indexed.emplace_back(idx, decrypt_shares(*kp, cr_.encryption));
-  }
+  for (auto& r : results) indexed.emplace_back(r.first, decrypt_shares(*kp, materialise(r.second)));
   auto masked = reconstruct_secrets(agg->committee_sharing_scheme, agg->vector_dimension, indexed);
   return RecipientOutput{agg->modulus, unmask(agg->masking_scheme, mask, masked)};
 }

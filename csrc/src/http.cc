@@ -423,6 +423,15 @@ HttpResponse opt_json(const std::optional<T>& v) {
   if (!v) return not_found_resource();
   return json_resp(wire::to_json(*v));
 }
+// A response whose JSON text exists already (the bulk downloads)
+HttpResponse opt_text(std::optional<std::string>&& text) {
+  if (!text) return not_found_resource();
+  HttpResponse r;
+  r.status = 200;
+  r.content_type = "application/json";
+  r.body = std::move(*text);
+  return r;
+}
 template <class T>
 HttpResponse vec_json(const std::vector<T>& v) {
   json::Value a = json::Value::array();
@@ -512,7 +521,7 @@ HttpResponse SdaHttpHandler::handle(const HttpRequest& req) {
       resp = empty(201);
     } else if (m == "GET" && is({"v1", "aggregations", "any", "jobs"})) {
       Agent c = caller(req);
-      resp = opt_json(svc_->get_clerking_job(c, c.id));
+      resp = opt_text(svc_->get_clerking_job_json(c, c.id));
     } else if (m == "POST" && is({"v1", "aggregations", "implied", "jobs", "*", "result"})) {
       svc_->create_clerking_result(caller(req), body_as<ClerkingResult>(req));
       resp = empty(201);
@@ -523,8 +532,8 @@ HttpResponse SdaHttpHandler::handle(const HttpRequest& req) {
     } else if (m == "GET" && is({"v1", "aggregations", "*", "status"})) {
       resp = opt_json(svc_->get_aggregation_status(caller(req), AggregationId::parse(seg[2])));
     } else if (m == "GET" && is({"v1", "aggregations", "*", "snapshots", "*", "result"})) {
-      resp = opt_json(svc_->get_snapshot_result(caller(req), AggregationId::parse(seg[2]),
-                                                SnapshotId::parse(seg[4])));
+      resp = opt_text(svc_->get_snapshot_result_json(caller(req), AggregationId::parse(seg[2]),
+                                                     SnapshotId::parse(seg[4])));
     } else if (m == "GET" && is({"v1", "aggregations", "*"})) {
       resp = opt_json(svc_->get_aggregation(caller(req), AggregationId::parse(seg[2])));
     } else if (m == "DELETE" && is({"v1", "aggregations", "*"})) {
@@ -619,12 +628,19 @@ SdaHttpClient::Reply SdaHttpClient::request(const std::string& method, const std
 
 std::optional<json::Value> SdaHttpClient::call(const std::string& method, const std::string& path,
                                                const Agent* caller, const std::string* body) {
+  auto text = call_text(method, path, caller, body);
+  if (!text) return std::nullopt;
+  return json::Value::parse(*text);
+}
+
+std::optional<std::string> SdaHttpClient::call_text(const std::string& method, const std::string& path,
+                                                    const Agent* caller, const std::string* body) {
   Reply r = request(method, path, caller, body);
   switch (r.status) {
     case 200:
     case 201:
       if (r.body.empty()) return std::nullopt;
-      return json::Value::parse(r.body);
+      return std::move(r.body);
     case 404:
       if (r.headers.count("resource-not-found")) return std::nullopt;
       throw SdaError("HTTP/REST route not found");
@@ -708,6 +724,15 @@ void SdaHttpClient::create_participation(const Agent& c, const Participation& p)
 }
 std::optional<ClerkingJob> SdaHttpClient::get_clerking_job(const Agent& c, const AgentId&) {
   return opt_from<ClerkingJob>(call("GET", "/v1/aggregations/any/jobs", &c, nullptr));
+}
+std::optional<std::string> SdaHttpClient::get_clerking_job_json(const Agent& c, const AgentId&) {
+  return call_text("GET", "/v1/aggregations/any/jobs", &c, nullptr);
+}
+std::optional<std::string> SdaHttpClient::get_snapshot_result_json(const Agent& c, const AggregationId& a,
+                                                                   const SnapshotId& s) {
+  auto text = call_text("GET", "/v1/aggregations/" + a.str() + "/snapshots/" + s.str() + "/result", &c, nullptr);
+  if (!text) throw SdaError("Missing response payload");
+  return text;
 }
 void SdaHttpClient::create_clerking_result(const Agent& c, const ClerkingResult& r) {
   std::string b = wire::encode(r);

@@ -105,11 +105,33 @@ bool Value::operator==(const Value& o) const {
   return false;
 }
 
-std::string escape_string(const std::string& s) {
-  std::string out;
-  out.reserve(s.size() + 2);
+namespace {
+// Bytes a string cannot hold verbatim: '"', '\\' and control characters. Long
+// strings (base64 payloads of megabytes) are copied in whole runs between them.
+struct PlainTable {
+  bool special[256];
+  PlainTable() {
+    for (int c = 0; c < 256; ++c) special[c] = c < 0x20 || c == '"' || c == '\\';
+  }
+};
+const PlainTable kPlain;
+
+inline size_t plain_run(const char* p, size_t n) {
+  size_t i = 0;
+  while (i < n && !kPlain.special[(unsigned char)p[i]]) ++i;
+  return i;
+}
+
+void escape_into(std::string& out, const std::string& s) {
   out.push_back('"');
-  for (unsigned char c : s) {
+  const char* p = s.data();
+  size_t n = s.size(), i = 0;
+  while (i < n) {
+    size_t run = plain_run(p + i, n - i);
+    out.append(p + i, run);
+    i += run;
+    if (i >= n) break;
+    unsigned char c = (unsigned char)p[i++];
     switch (c) {
       case '"': out += "\\\""; break;
       case '\\': out += "\\\\"; break;
@@ -118,17 +140,21 @@ std::string escape_string(const std::string& s) {
       case '\t': out += "\\t"; break;
       case '\b': out += "\\b"; break;
       case '\f': out += "\\f"; break;
-      default:
-        if (c < 0x20) {
-          char buf[8];
-          std::snprintf(buf, sizeof(buf), "\\u%04x", c);
-          out += buf;
-        } else {
-          out.push_back((char)c);
-        }
+      default: {
+        char buf[8];
+        std::snprintf(buf, sizeof(buf), "\\u%04x", c);
+        out += buf;
+      }
     }
   }
   out.push_back('"');
+}
+}  // namespace
+
+std::string escape_string(const std::string& s) {
+  std::string out;
+  out.reserve(s.size() + 2);
+  escape_into(out, s);
   return out;
 }
 
@@ -145,7 +171,7 @@ void Value::dump_to(std::string& out) const {
       if (!std::strpbrk(buf, ".eE")) out += ".0";
       break;
     }
-    case Type::String: out += escape_string(s_); break;
+    case Type::String: escape_into(out, s_); break;
     case Type::Array: {
       out.push_back('[');
       bool first = true;
@@ -163,7 +189,7 @@ void Value::dump_to(std::string& out) const {
       for (auto& kv : *o_) {
         if (!first) out.push_back(',');
         first = false;
-        out += escape_string(kv.first);
+        escape_into(out, kv.first);
         out.push_back(':');
         kv.second.dump_to(out);
       }
@@ -173,8 +199,30 @@ void Value::dump_to(std::string& out) const {
   }
 }
 
+namespace {
+// Lower bound of the dumped size (payload strings dominate): one allocation
+// instead of a doubling chain over hundreds of megabytes.
+size_t dump_estimate(const Value& v) {
+  switch (v.type()) {
+    case Value::Type::String: return v.as_string().size() + 2;
+    case Value::Type::Array: {
+      size_t n = 2;
+      for (auto& x : v.as_array()) n += dump_estimate(x) + 1;
+      return n;
+    }
+    case Value::Type::Object: {
+      size_t n = 2;
+      for (auto& kv : v.as_object()) n += kv.first.size() + 4 + dump_estimate(kv.second);
+      return n;
+    }
+    default: return 8;
+  }
+}
+}  // namespace
+
 std::string Value::dump() const {
   std::string s;
+  s.reserve(dump_estimate(*this));
   dump_to(s);
   return s;
 }
@@ -231,11 +279,17 @@ struct Parser {
     ++i;
     std::string out;
     while (true) {
+      // whole runs of plain bytes at once (payload strings are megabytes long)
+      size_t run = plain_run(t.data() + i, t.size() - i);
+      if (run) {
+        if (out.empty()) out.reserve(run);
+        out.append(t.data() + i, run);
+        i += run;
+      }
       if (i >= t.size()) fail("unterminated string");
       char c = t[i++];
       if (c == '"') break;
       if ((unsigned char)c < 0x20) fail("control character in string");
-      if (c != '\\') { out.push_back(c); continue; }
       if (i >= t.size()) fail("bad escape");
       char e = t[i++];
       switch (e) {

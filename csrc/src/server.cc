@@ -102,6 +102,12 @@ std::optional<ClerkingJob> SdaServer::poll_clerking_job(const AgentId& clerk) {
 std::optional<ClerkingJob> SdaServer::get_clerking_job(const AgentId& clerk, const ClerkingJobId& job) {
   return s_.clerking_jobs->get_clerking_job(clerk, job);
 }
+std::optional<std::string> SdaServer::poll_clerking_job_json(const AgentId& clerk) {
+  return s_.clerking_jobs->poll_clerking_job_json(clerk);
+}
+std::optional<ClerkingJob> SdaServer::get_clerking_job_head(const AgentId& clerk, const ClerkingJobId& job) {
+  return s_.clerking_jobs->get_clerking_job_head(clerk, job);
+}
 void SdaServer::create_clerking_result(const ClerkingResult& r) { s_.clerking_jobs->create_clerking_result(r); }
 
 std::optional<SnapshotResult> SdaServer::get_snapshot_result(const AggregationId& a, const SnapshotId& s) {
@@ -115,6 +121,27 @@ std::optional<SnapshotResult> SdaServer::get_snapshot_result(const AggregationId
   r.number_of_participations = s_.aggregations->count_participations_snapshot(a, s);
   r.recipient_encryptions = s_.aggregations->get_snapshot_mask(s);
   return r;
+}
+
+// The same document assembled from the stores' text: the mask boxes (one per
+// participation) and the results are spliced in as they are stored.
+std::optional<std::string> SdaServer::get_snapshot_result_json(const AggregationId& a, const SnapshotId& s) {
+  std::string out = "{\"snapshot\":" + wire::to_json(s).dump() + ",\"number_of_participations\":" +
+                    std::to_string(s_.aggregations->count_participations_snapshot(a, s)) +
+                    ",\"clerk_encryptions\":[";
+  bool first = true;
+  for (auto& job : s_.clerking_jobs->list_results(s)) {
+    auto res = s_.clerking_jobs->get_result_json(s, job);
+    if (!res) throw SdaError("inconsistent storage");
+    if (!first) out.push_back(',');
+    first = false;
+    out += *res;
+  }
+  out += "],\"recipient_encryptions\":";
+  auto masks = s_.aggregations->get_snapshot_mask_json(s);
+  out += masks ? *masks : std::string("null");
+  out.push_back('}');
+  return out;
 }
 
 void SdaServer::upsert_auth_token(const AuthToken& t) { s_.auth_tokens->upsert_auth_token(t); }
@@ -178,9 +205,14 @@ std::optional<ClerkingJob> SdaServerService::get_clerking_job(const Agent& calle
   acl_agent_is(caller, clerk);
   return srv_->poll_clerking_job(clerk);
 }
+std::optional<std::string> SdaServerService::get_clerking_job_json(const Agent& caller, const AgentId& clerk) {
+  acl_agent_is(caller, clerk);
+  return srv_->poll_clerking_job_json(clerk);
+}
 void SdaServerService::create_clerking_result(const Agent& caller, const ClerkingResult& r) {
-  // re-fetch the job by (clerk, job) so a forged clerk id cannot be used (server.rs:351-360)
-  auto job = srv_->get_clerking_job(r.clerk, r.job);
+  // re-fetch the job by (clerk, job) so a forged clerk id cannot be used (server.rs:351-360);
+  // only its head is read
+  auto job = srv_->get_clerking_job_head(r.clerk, r.job);
   if (!job) throw SdaError("Job not found");
   acl_agent_is(caller, job->clerk);
   srv_->create_clerking_result(r);
@@ -217,6 +249,15 @@ std::optional<SnapshotResult> SdaServerService::get_snapshot_result(const Agent&
   auto snap = srv_->stores().aggregations->get_snapshot(a, s);
   if (!snap || snap->aggregation != a) return std::nullopt;
   return srv_->get_snapshot_result(a, s);
+}
+
+std::optional<std::string> SdaServerService::get_snapshot_result_json(const Agent& caller,
+                                                                     const AggregationId& a,
+                                                                     const SnapshotId& s) {
+  acl_agent_is(caller, require_aggregation(a).recipient);
+  auto snap = srv_->stores().aggregations->get_snapshot(a, s);
+  if (!snap || snap->aggregation != a) return std::nullopt;
+  return srv_->get_snapshot_result_json(a, s);
 }
 
 std::shared_ptr<SdaServerService> new_memory_server() {

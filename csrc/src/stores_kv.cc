@@ -324,6 +324,9 @@ class KvAggregationsStore : public AggregationsStore {
     if (prev && json::Value::parse(*prev) != arr) throw SdaError("File already exists");
     masks_->put(s.str(), arr.dump());
   }
+  std::optional<std::string> get_snapshot_mask_json(const SnapshotId& s) override {
+    return masks_->get(s.str());
+  }
   std::optional<std::vector<Encryption>> get_snapshot_mask(const SnapshotId& s) override {
     auto v = masks_->get(s.str());
     if (!v) return std::nullopt;
@@ -357,14 +360,31 @@ class KvClerkingJobsStore : public ClerkingJobsStore {
   std::optional<ClerkingJob> get_clerking_job(const AgentId& clerk, const ClerkingJobId& job) override {
     return get_as<ClerkingJob>(*f_("jobs/queue/" + clerk.str()), job.str());
   }
+  std::optional<std::string> poll_clerking_job_json(const AgentId& clerk) override {
+    auto all = f_("jobs/queue/" + clerk.str())->all();
+    if (all.empty()) return std::nullopt;
+    return std::move(all.front().second);
+  }
+  std::optional<ClerkingJob> get_clerking_job_head(const AgentId& clerk, const ClerkingJobId& job) override {
+    auto text = f_("jobs/queue/" + clerk.str())->get(job.str());
+    if (!text) return std::nullopt;
+    if (auto view = wire::scan_clerking_job(*text)) return view->head;
+    return wire::decode<ClerkingJob>(*text);
+  }
+  std::optional<std::string> get_result_json(const SnapshotId& snapshot, const ClerkingJobId& job) override {
+    return f_("jobs/results/" + snapshot.str())->get(job.str());
+  }
   void create_clerking_result(const ClerkingResult& r) override {
-    // atomic queue -> done move (the reference's check-then-write was racy)
+    // atomic queue -> done move (the reference's check-then-write was racy); the job
+    // moves as the text it is stored as
     std::lock_guard<std::mutex> g(mu_);
     auto queue = f_("jobs/queue/" + r.clerk.str());
-    auto job = get_as<ClerkingJob>(*queue, r.job.str());
-    if (!job) throw SdaError("Job not found");
-    upsert_with_id(*f_("jobs/results/" + job->snapshot.str()), r.job.str(), r);
-    upsert_with_id(*f_("jobs/done/" + r.clerk.str()), r.job.str(), *job);
+    auto text = queue->get(r.job.str());
+    if (!text) throw SdaError("Job not found");
+    auto view = wire::scan_clerking_job(*text);
+    const SnapshotId snapshot = view ? view->head.snapshot : wire::decode<ClerkingJob>(*text).snapshot;
+    upsert_with_id(*f_("jobs/results/" + snapshot.str()), r.job.str(), r);
+    f_("jobs/done/" + r.clerk.str())->put(r.job.str(), *text);
     queue->remove(r.job.str());
   }
   std::vector<ClerkingJobId> list_results(const SnapshotId& snapshot) override {
@@ -403,6 +423,29 @@ std::vector<std::vector<Encryption>> AggregationsStore::snapshot_clerk_jobs_data
       shares[ix].push_back(std::move(p.clerk_encryptions[ix].second));
   }
   return shares;
+}
+
+std::optional<std::string> AggregationsStore::get_snapshot_mask_json(const SnapshotId& snapshot) {
+  auto m = get_snapshot_mask(snapshot);
+  if (!m) return std::nullopt;
+  json::Value arr = json::Value::array();
+  for (auto& e : *m) arr.push(wire::to_json(e));
+  return arr.dump();
+}
+std::optional<std::string> ClerkingJobsStore::poll_clerking_job_json(const AgentId& clerk) {
+  auto j = poll_clerking_job(clerk);
+  if (!j) return std::nullopt;
+  return wire::encode(*j);
+}
+std::optional<ClerkingJob> ClerkingJobsStore::get_clerking_job_head(const AgentId& clerk,
+                                                                    const ClerkingJobId& job) {
+  return get_clerking_job(clerk, job);
+}
+std::optional<std::string> ClerkingJobsStore::get_result_json(const SnapshotId& snapshot,
+                                                              const ClerkingJobId& job) {
+  auto r = get_result(snapshot, job);
+  if (!r) return std::nullopt;
+  return wire::encode(*r);
 }
 
 std::shared_ptr<Collection> make_mem_collection() { return std::make_shared<MemCollection>(); }

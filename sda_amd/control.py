@@ -386,8 +386,17 @@ class SdaClient:
         return [json.loads(t) for t in
                 self._h.new_participations([list(v) for v in vectors], aggregation_id)]
 
-    def participate_many(self, vectors: Sequence[Sequence[int]], aggregation_id: str) -> None:
-        self._h.participate_many([list(v) for v in vectors], aggregation_id)
+    def participate_many(self, vectors, aggregation_id: str) -> None:
+        """`vectors`: a sequence of integer sequences, or a [P][D] numpy array."""
+        if hasattr(vectors, "ndim"):
+            self._h.participate_array(vectors, aggregation_id)
+        else:
+            self._h.participate_many([list(v) for v in vectors], aggregation_id)
+
+    def role_timings(self) -> Dict[str, float]:
+        """Milliseconds of the last clerk_once / reveal_aggregation: fetch (service
+        calls: HTTP, JSON, base64), process (the cryptography), post."""
+        return dict(self._h.role_timings())
 
     # clerking
     def clerk_once(self) -> bool:

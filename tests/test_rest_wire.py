@@ -270,3 +270,97 @@ def test_client_filestore(tmp_path, native):
     assert (tmp_path / "ks" / "thing.json").exists()
     assert (tmp_path / "ks" / "alias_agent.json").exists()
     assert ks.get("missing") is None
+
+
+# ---- bulk downloads: response text and zero-copy views ---------------------------------
+def new_full_agent(service):
+    ag = C.fake_agent()
+    service.create_agent(ag, ag)
+    key = C.fake_key_for(ag)
+    service.create_encryption_key(ag, key)
+    return ag, key
+
+
+def _bulk_fixture(service, masked):
+    """A snapshotted aggregation with 5 fake participations; returns
+    (recipient agent, aggregation, clerks)."""
+    import os as _os
+
+    recipient, rkey = new_full_agent(service)
+    kw = dict(masking_scheme=C.masking_full(13)) if masked else {}
+    agg = C.aggregation("bulk", 4, 13, recipient["id"], rkey["body"]["id"],
+                        committee_sharing_scheme=C.sharing_additive(3, 13), **kw)
+    service.create_aggregation(recipient, agg)
+    clerks = [new_full_agent(service) for _ in range(3)]
+    service.create_committee(recipient, C.committee(
+        agg["id"], [(a["id"], k["body"]["id"]) for a, k in clerks]))
+    for i in range(5):
+        part, _ = new_full_agent(service)
+        service.create_participation(part, {
+            "id": C.new_id(), "participant": part["id"], "aggregation": agg["id"],
+            "recipient_encryption": C.sodium(_os.urandom(70)) if masked else None,
+            "clerk_encryptions": [[a["id"], C.sodium(_os.urandom(50 + i))] for a, _ in clerks]})
+    service.create_snapshot(recipient, C.snapshot(agg["id"]))
+    return recipient, agg, clerks
+
+
+@pytest.mark.parametrize("kind", ["memory", "jfs", "document", "http-jfs"])
+@pytest.mark.parametrize("masked", [False, True])
+def test_bulk_downloads_as_text_equal_the_struct_forms(native, tmp_path, kind, masked):
+    """`get_clerking_job_json` / `get_snapshot_result_json` carry the same
+    document as the struct forms (ClerkingJob protocol/src/resources.rs:127-139,
+    SnapshotResult :178-188), and the views locate every box in the text."""
+    server = {"memory": C.memory_server, "jfs": lambda: C.jfs_server(str(tmp_path / "j")),
+              "document": lambda: C.document_server(str(tmp_path / "d")),
+              "http-jfs": lambda: C.jfs_server(str(tmp_path / "hj"))}[kind]()
+    http = C.HttpServer(server).start() if kind.startswith("http") else None
+    try:
+        service = C.http_client(http.root, C.MemoryStore()) if http else server
+        recipient, agg, clerks = _bulk_fixture(service, masked)
+        clerk = clerks[1][0]
+        job = service.get_clerking_job(clerk, clerk["id"])
+        text = service.handle.get_clerking_job_json(json.dumps(clerk), clerk["id"])
+        assert json.loads(text) == job
+        head, spans = C._c().scan_clerking_job(text)
+        assert json.loads(head) == dict(job, encryptions=[])
+        assert [text[o:o + n] for o, n in spans] == [e["Sodium"] for e in job["encryptions"]]
+        # results + masks
+        for a, _ in clerks:
+            j = service.get_clerking_job(a, a["id"])
+            service.create_clerking_result(a, {"job": j["id"], "clerk": a["id"],
+                                               "encryption": C.sodium(b"r" * 60)})
+        snap = service.get_aggregation_status(recipient, agg["id"])["snapshots"][0]["id"]
+        res = service.get_snapshot_result(recipient, agg["id"], snap)
+        rtext = service.handle.get_snapshot_result_json(json.dumps(recipient), agg["id"], snap)
+        assert json.loads(rtext) == res
+        sid, count, results, has_masks, masks = C._c().scan_snapshot_result(rtext)
+        assert sid == snap and count == 5 and has_masks == masked
+        assert [(j, c, rtext[o:o + n]) for j, c, o, n in results] == \
+            [(r["job"], r["clerk"], r["encryption"]["Sodium"]) for r in res["clerk_encryptions"]]
+        assert [rtext[o:o + n] for o, n in masks] == \
+            [e["Sodium"] for e in (res["recipient_encryptions"] or [])]
+        # the ACLs of the struct forms hold for the text forms
+        stranger, _ = new_full_agent(service)
+        with pytest.raises(C.errors.PermissionDenied):
+            service.handle.get_snapshot_result_json(json.dumps(stranger), agg["id"], snap)
+    finally:
+        if http:
+            http.stop()
+
+
+def test_views_accept_whitespace_and_reject_what_they_cannot_locate(native):
+    scan = C._c().scan_clerking_job
+    ids = {k: C.new_id() for k in ("id", "clerk", "aggregation", "snapshot")}
+    plain = json.dumps(dict(ids, encryptions=[{"Sodium": "QUJD"}, {"Sodium": ""}]))
+    head, spans = scan(plain)
+    assert json.loads(head)["clerk"] == ids["clerk"] and [n for _, n in spans] == [4, 0]
+    pretty = json.dumps(dict(ids, encryptions=[{"Sodium": "QUJD"}]), indent=2)
+    assert scan(pretty) is not None
+    reordered = json.dumps(dict(encryptions=[{"Sodium": "QUJD"}], **ids))
+    assert scan(reordered) is not None
+    # outside the plain shape: the caller falls back to the full codec
+    assert scan(plain.replace("QUJD", "QU\\u004aD")) is None      # an escape inside a payload
+    assert scan(json.dumps(dict(ids, encryptions=[{"Other": "QUJD"}]))) is None
+    assert scan(json.dumps(ids)) is None                           # a field is missing
+    assert scan(plain + "x") is None and scan(plain[:-1]) is None
+    assert scan(json.dumps(dict(ids, extra=1, encryptions=[]))) is None
