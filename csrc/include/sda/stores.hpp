@@ -124,6 +124,12 @@ class Collection {
   virtual bool remove(const std::string& id) = 0;
   // all (id, json) sorted by id (jfs::Store::all is a BTreeMap)
   virtual std::vector<std::pair<std::string, std::string>> all() = 0;
+  // the entry with the smallest id (what `all().front()` is), without copying the rest
+  virtual std::optional<std::pair<std::string, std::string>> first() {
+    auto a = all();
+    if (a.empty()) return std::nullopt;
+    return std::move(a.front());
+  }
   virtual size_t count() = 0;
 };
 std::shared_ptr<Collection> make_mem_collection();

@@ -148,9 +148,23 @@ ReadStatus read_message(int fd, std::string& buf, std::string& head, std::string
     }
   } else if (has_len) {
     if (clen > max_body) return ReadStatus::TooLarge;
-    if (!fill(clen)) return ReadStatus::Closed;
-    body = buf.substr(0, clen);
-    buf.erase(0, clen);
+    if (buf.size() >= clen) {
+      body = buf.substr(0, clen);
+      buf.erase(0, clen);
+    } else {
+      // a long body (bulk uploads and downloads reach hundreds of megabytes) is
+      // received straight into its final storage: one allocation, no staging copy
+      size_t have = buf.size();
+      body.swap(buf);
+      buf.clear();
+      body.resize(clen);
+      while (have < clen) {
+        ssize_t r = ::recv(fd, &body[have], clen - have, 0);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) return ReadStatus::Closed;
+        have += (size_t)r;
+      }
+    }
   } else if (is_response) {
     char tmp[1 << 16];
     while (true) {

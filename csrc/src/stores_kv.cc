@@ -67,6 +67,11 @@ class MemCollection : public Collection {
     std::lock_guard<std::mutex> g(mu_);
     return {m_.begin(), m_.end()};
   }
+  std::optional<std::pair<std::string, std::string>> first() override {
+    std::lock_guard<std::mutex> g(mu_);
+    if (m_.empty()) return std::nullopt;
+    return *m_.begin();
+  }
   size_t count() override {
     std::lock_guard<std::mutex> g(mu_);
     return m_.size();
@@ -82,11 +87,13 @@ class FileCollection : public Collection {
   explicit FileCollection(std::string dir) : dir_(std::move(dir)) { mkdirs(dir_); }
   std::optional<std::string> get(const std::string& id) override {
     if (!safe_id(id)) throw SdaError("store: invalid id " + id);
-    std::ifstream f(path(id), std::ios::binary);
+    std::ifstream f(path(id), std::ios::binary | std::ios::ate);
     if (!f) return std::nullopt;
-    std::stringstream ss;
-    ss << f.rdbuf();
-    return ss.str();
+    std::string text((size_t)std::max<std::streamoff>(0, f.tellg()), '\0');  // one read, no stream copy
+    f.seekg(0);
+    f.read(&text[0], (std::streamsize)text.size());
+    text.resize((size_t)f.gcount());
+    return text;
   }
   void put(const std::string& id, const std::string& json) override {
     if (!safe_id(id)) throw SdaError("store: invalid id " + id);
@@ -110,6 +117,13 @@ class FileCollection : public Collection {
       if (v) out.emplace_back(id, *v);
     }
     return out;
+  }
+  std::optional<std::pair<std::string, std::string>> first() override {
+    for (auto& id : ids()) {
+      auto v = get(id);
+      if (v) return std::make_pair(id, std::move(*v));
+    }
+    return std::nullopt;
   }
   size_t count() override { return ids().size(); }
 
@@ -353,17 +367,17 @@ class KvClerkingJobsStore : public ClerkingJobsStore {
     create_with_id(*f_("jobs/queue/" + j.clerk.str()), j.id.str(), j);
   }
   std::optional<ClerkingJob> poll_clerking_job(const AgentId& clerk) override {
-    auto all = f_("jobs/queue/" + clerk.str())->all();
-    if (all.empty()) return std::nullopt;
-    return wire::decode<ClerkingJob>(all.front().second);
+    auto head = f_("jobs/queue/" + clerk.str())->first();
+    if (!head) return std::nullopt;
+    return wire::decode<ClerkingJob>(head->second);
   }
   std::optional<ClerkingJob> get_clerking_job(const AgentId& clerk, const ClerkingJobId& job) override {
     return get_as<ClerkingJob>(*f_("jobs/queue/" + clerk.str()), job.str());
   }
   std::optional<std::string> poll_clerking_job_json(const AgentId& clerk) override {
-    auto all = f_("jobs/queue/" + clerk.str())->all();
-    if (all.empty()) return std::nullopt;
-    return std::move(all.front().second);
+    auto head = f_("jobs/queue/" + clerk.str())->first();
+    if (!head) return std::nullopt;
+    return std::move(head->second);
   }
   std::optional<ClerkingJob> get_clerking_job_head(const AgentId& clerk, const ClerkingJobId& job) override {
     auto text = f_("jobs/queue/" + clerk.str())->get(job.str());

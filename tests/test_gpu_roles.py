@@ -163,7 +163,10 @@ def test_clerk_job_gpu_equals_cpu(tmp_path, native, cuda):
         p.upload_agent()
         p.participate([rng.randrange(m) for _ in range(D)], agg["id"])
     recipient.end_aggregation(agg["id"])
-    cl = clerks[0]
+    # the committee is drafted from every key holder (the recipient has a key too):
+    # take a clerk that was
+    drafted = [c for c, _ in server.get_committee(recipient.agent, agg["id"])["clerks_and_keys"]]
+    cl = next(c for c in clerks if c.id in drafted)
     job = server.get_clerking_job(cl.agent, cl.id)
     assert job is not None and len(job["encryptions"]) == 6
     cpu = cl.process_clerking_job(job)
