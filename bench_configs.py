@@ -13,6 +13,9 @@ JSON line each (rank 0).
               MFMA GEMM
   --config 7  config 5 over a prime below 256 (u8 share storage)
   --config 8  16 x 1M per GPU, the reference's PSS_155_19682_100 (19,682 clerks)
+  --config 9  config 2 with a full mask (masks sealed for the recipient)
+  --config 10 config 2 with a ChaCha mask (rand-0.3 seed expansion on both sides)
+  --config 11 config 10 over m = 2^31 - 1
 
 Multi-GPU: python bench_configs.py --config 3 --gpus N   (starts its own N ranks), or
            python -m torch.distributed.run --nproc-per-node N bench_configs.py --config 3 --gpus N
@@ -36,7 +39,7 @@ if ROOT not in sys.path:
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 3, 4, 5, 6, 7, 8])
+    ap.add_argument("--config", type=int, required=True, choices=list(range(1, 12)))
     ap.add_argument("--gpus", type=int, default=0,
                     help="ranks (one per GPU). > 1 from a plain command line: the script starts "
                          "them itself through torch.distributed.run. 0 = whatever the launcher "
@@ -220,7 +223,7 @@ def gpu_configs(args):
               "metric": "aggregated secret-shared elements/sec", "unit": "elements/s",
               "value": P * world * D / (ms / 1e3), "ms_per_round": ms, "steps": steps,
               "n_gpus": world, "participants": P * world, "dimension": D,
-              "sharing": spec.sharing.to_wire(),
+              "sharing": spec.sharing.to_wire(), "masking": spec.masking.to_wire(),
               "clerks_used": clerks or f"all {spec.n_clerks}",
               "pss_backend": ("mfma" if eng._pss_mfma else "valu") if eng._pss is not None else None,
               "share_storage": str(eng.vdtype).replace("torch.", ""),

@@ -606,7 +606,11 @@ std::vector<int64_t> Backend::reveal(const Aggregation& agg, const EncryptionKey
       Keys km = open_setup(mem, ma, kidx_m, sks, pks, err);
       uint32_t* seeds = mem.take<uint32_t>((size_t)ma.M * w);
       open_data(mem, ma, km, seeds, err);
-      launch_chacha_mask_sum(ma.M, (int)D, m, w, seeds, mask_sum, err, s_);
+      const int groups = chacha_sum_groups(ma.M, (int)D);
+      uint32_t* part = mem.take<uint32_t>((size_t)groups * D);
+      uint32_t* scratch = mem.take<uint32_t>(chacha_scratch_words(ma.M, (int)D));
+      uint64_t* fix = mem.take<uint64_t>(D);
+      launch_chacha_mask_sum(ma.M, (int)D, m, w, seeds, mask_sum, part, groups, scratch, fix, err, s_);
       launched("chacha_mask_sum");
     }
     out = mem.take<uint32_t>(D);
@@ -699,28 +703,43 @@ DeviceParticipations Backend::participate_many(const Aggregation& agg,
     const RngKeyArg rng = fresh_rng_key();
     void* shares = mem.take<uint8_t>((size_t)n * P * B * value_bytes);
     uint32_t* cnt = mem.take<uint32_t>((size_t)n * P * tiles(B));
-    uint32_t* mask_out = mask_mode == kMaskFull ? mem.take<uint32_t>((size_t)P * D) : nullptr;
+    // full masks in the shares' storage type (32-bit ahead of the limb GEMM)
+    const int mask_bytes = (pss && big) ? 4 : value_bytes;
+    void* mask_out = mask_mode == kMaskFull ? mem.take<uint8_t>((size_t)P * D * mask_bytes) : nullptr;
     uint32_t* mask_cnt = mask_mode == kMaskFull ? mem.take<uint32_t>((size_t)P * tiles(D)) : nullptr;
     uint32_t* seeds = mask_mode == kMaskChaCha ? mem.take<uint32_t>((size_t)P * seed_words) : nullptr;
     bool have_cnt = true, have_mask_cnt = mask_mode == kMaskFull;
+    int share_mode = mask_mode;
+    if (mask_mode == kMaskChaCha) {
+      // chacha.rs:29-45 as a pre-pass: fresh seeds, masked = secret + the seed's stream;
+      // the shares then come from the unmasked fast kernels
+      launch_chacha_seeds(P, seed_words, rng, 0, seeds, s_);
+      launched("chacha_seeds");
+      int32_t* msk = mem.take<int32_t>((size_t)P * D);
+      uint32_t* scratch = mem.take<uint32_t>(chacha_scratch_words(P, (int)D));
+      launch_chacha_mask_apply(P, (int)D, m, seed_words, seeds, secrets, msk, scratch, err, s_);
+      launched("chacha_mask_apply");
+      secrets = msk;
+      share_mode = kMaskNone;
+    }
     if (!pss) {
-      launch_share_additive(P, (int)D, n, m, value_bytes, secrets, mask_mode, seed_words, rng, 0, shares,
-                            cnt, mask_out, mask_cnt, seeds, err, s_);
+      launch_share_additive(P, (int)D, n, m, value_bytes, secrets, share_mode, rng, 0, shares, cnt,
+                            mask_out, mask_cnt, s_);
       launched("share_additive");
     } else if (!big) {
       uint32_t* dM = to_device(mem, share_matrix);
-      launch_share_pss(P, (int)D, n, (int)k, t_priv, m, value_bytes, secrets, dM, mask_mode, seed_words,
-                       rng, 0, shares, cnt, mask_out, nullptr, seeds, err, s_);
+      launch_share_pss(P, (int)D, n, (int)k, t_priv, m, value_bytes, secrets, dM, share_mode, rng, 0,
+                       shares, cnt, mask_out, nullptr, s_);
       launched("share_pss");
       have_mask_cnt = false;  // packed batches do not align with the mask tiles: recounted
       sync();
     } else {
       const int32_t* masked = secrets;
-      if (mask_mode != kMaskNone) {
+      if (share_mode == kMaskFull) {
         int32_t* msk = mem.take<int32_t>((size_t)P * D);
         uint32_t* c1 = mem.take<uint32_t>((size_t)P * tiles(D));
-        launch_share_additive(P, (int)D, 1, m, 4, secrets, mask_mode, seed_words, rng, 0, msk, c1,
-                              mask_out, mask_cnt, seeds, err, s_);
+        launch_share_additive(P, (int)D, 1, m, 4, secrets, kMaskFull, rng, 0, msk, c1, mask_out,
+                              mask_cnt, s_);
         launched("mask_secrets");
         masked = msk;
       }
@@ -759,8 +778,8 @@ DeviceParticipations Backend::participate_many(const Aggregation& agg,
       uint32_t* kidx_m = zeros(mem, P);
       uint32_t* pks_r = key_words(mem, {recipient_key->sodium.data()});
       Keys km = seal_setup(mem, marena, kidx_m, pks_r, (uint64_t)n * P, rng, err);
-      seal_data(mem, marena, km, full ? (const void*)mask_out : (const void*)seeds, 4,
-                have_mask_cnt ? mask_cnt : nullptr, err);
+      seal_data(mem, marena, km, full ? (const void*)mask_out : (const void*)seeds,
+                full ? mask_bytes : 4, have_mask_cnt ? mask_cnt : nullptr, err);
     }
     check(err, "participate");
     t.mark("gpu");

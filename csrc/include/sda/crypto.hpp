@@ -74,6 +74,12 @@ class ChaChaRng {
   int index_;
 };
 
+// Test hook: cap the acceptance zone of ChaChaRng::gen_range (draws at or above
+// cap - cap % range are rejected), so that rejections -- at most 1e-10 per draw for
+// 31-bit moduli -- can be made frequent; the device kernels have the same hook
+// (kernels.hpp). UINT64_MAX = no cap. Process-wide.
+void set_chacha_zone_cap(uint64_t cap);
+
 // ---- Poly1305 --------------------------------------------------------------
 void poly1305(uint8_t tag[16], const uint8_t* msg, size_t n, const uint8_t key[32]);
 bool verify16(const uint8_t a[16], const uint8_t b[16]);

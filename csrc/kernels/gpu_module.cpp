@@ -91,27 +91,30 @@ PYBIND11_MODULE(_sda_gpu, m) {
   });
   m.def("share_additive",
         [](int Pn, int D, int n, uint32_t mod, int value_bytes, uintptr_t secrets, int mask_mode,
-           int seed_words, std::vector<uint32_t> rng, uint64_t owner_base, uintptr_t shares,
-           uintptr_t cnt, uintptr_t mask_out, uintptr_t mask_cnt, uintptr_t seeds, uintptr_t err,
-           uintptr_t stream) {
+           std::vector<uint32_t> rng, uint64_t owner_base, uintptr_t shares, uintptr_t cnt,
+           uintptr_t mask_out, uintptr_t mask_cnt, uintptr_t stream) {
           if (n < 1 || n > 256) throw std::invalid_argument("share_additive: n must be 1..256");
+          if (mask_mode != kMaskNone && mask_mode != kMaskFull)
+            throw std::invalid_argument("share_additive: mask mode none or full (ChaCha masks are "
+                                        "applied first: chacha_mask_apply)");
           launch_share_additive(Pn, D, n, mod, value_bytes, P<const int32_t>(secrets), mask_mode,
-                                seed_words, rng_from(rng), owner_base, P<void>(shares),
-                                P<uint32_t>(cnt), P<uint32_t>(mask_out), P<uint32_t>(mask_cnt),
-                                P<uint32_t>(seeds), P<uint32_t>(err), S(stream));
+                                rng_from(rng), owner_base, P<void>(shares), P<uint32_t>(cnt),
+                                P<void>(mask_out), P<uint32_t>(mask_cnt), S(stream));
           check_launch("share_additive");
         });
   m.def("share_pss",
         [](int Pn, int D, int n, int k, int t, uint32_t prime, int value_bytes, uintptr_t secrets,
-           uintptr_t matrix, int mask_mode, int seed_words, std::vector<uint32_t> rng,
-           uint64_t owner_base, uintptr_t shares, uintptr_t cnt, uintptr_t mask_out,
-           uintptr_t mask_cnt, uintptr_t seeds, uintptr_t err, uintptr_t stream) {
+           uintptr_t matrix, int mask_mode, std::vector<uint32_t> rng, uint64_t owner_base,
+           uintptr_t shares, uintptr_t cnt, uintptr_t mask_out, uintptr_t mask_cnt,
+           uintptr_t stream) {
           if (k > 8 || t > 16 || n > 64)
             throw std::invalid_argument("share_pss: register kernel supports k<=8, t<=16, n<=64");
+          if (mask_mode != kMaskNone && mask_mode != kMaskFull)
+            throw std::invalid_argument("share_pss: mask mode none or full");
           launch_share_pss(Pn, D, n, k, t, prime, value_bytes, P<const int32_t>(secrets),
-                           P<const uint32_t>(matrix), mask_mode, seed_words, rng_from(rng),
-                           owner_base, P<void>(shares), P<uint32_t>(cnt), P<uint32_t>(mask_out),
-                           P<uint32_t>(mask_cnt), P<uint32_t>(seeds), P<uint32_t>(err), S(stream));
+                           P<const uint32_t>(matrix), mask_mode, rng_from(rng), owner_base,
+                           P<void>(shares), P<uint32_t>(cnt), P<void>(mask_out),
+                           P<uint32_t>(mask_cnt), S(stream));
           check_launch("share_pss");
         });
   m.def("set_share16", &set_share16, "use the 16-bit-draw additive share kernel (benchmarking)");
@@ -122,9 +125,33 @@ PYBIND11_MODULE(_sda_gpu, m) {
     launch_count(M, L, value_bytes, P<const void>(vals), P<uint32_t>(cnt), S(stream));
     check_launch("count");
   });
+  m.def("chacha_seeds", [](int Pn, int seed_words, std::vector<uint32_t> rng, uint64_t owner_base,
+                           uintptr_t seeds, uintptr_t stream) {
+    if (seed_words < 1 || seed_words > 8) throw std::invalid_argument("chacha_seeds: 1..8 words");
+    launch_chacha_seeds(Pn, seed_words, rng_from(rng), owner_base, P<uint32_t>(seeds), S(stream));
+    check_launch("chacha_seeds");
+  });
+  m.def("chacha_scratch_words", &chacha_scratch_words);
+  m.def("chacha_sum_groups", &chacha_sum_groups);
+  m.def("set_chacha_zone_cap", &set_chacha_zone_cap,
+        "test hook: cap the rand-0.3 acceptance zone (2^64 - 1 = none)");
+  m.def("chacha_mask_apply", [](int Pn, int D, uint32_t mod, int seed_words, uintptr_t seeds,
+                                uintptr_t secrets, uintptr_t masked, uintptr_t scratch,
+                                uintptr_t err, uintptr_t stream) {
+    if (mod < 2 || seed_words < 1 || seed_words > 8)
+      throw std::invalid_argument("chacha_mask_apply: modulus >= 2, seeds of 1..8 words");
+    launch_chacha_mask_apply(Pn, D, mod, seed_words, P<const uint32_t>(seeds),
+                             P<const int32_t>(secrets), P<int32_t>(masked), P<uint32_t>(scratch),
+                             P<uint32_t>(err), S(stream));
+    check_launch("chacha_mask_apply");
+  });
   m.def("chacha_mask_sum", [](int Pn, int D, uint32_t mod, int seed_words, uintptr_t seeds,
-                              uintptr_t out, uintptr_t err, uintptr_t stream) {
+                              uintptr_t out, uintptr_t part, int groups, uintptr_t scratch,
+                              uintptr_t fix, uintptr_t err, uintptr_t stream) {
+    if (mod < 2 || seed_words < 1 || seed_words > 8 || groups < 1)
+      throw std::invalid_argument("chacha_mask_sum: modulus >= 2, seeds of 1..8 words");
     launch_chacha_mask_sum(Pn, D, mod, seed_words, P<const uint32_t>(seeds), P<uint32_t>(out),
+                           P<uint32_t>(part), groups, P<uint32_t>(scratch), P<uint64_t>(fix),
                            P<uint32_t>(err), S(stream));
     check_launch("chacha_mask_sum");
   });

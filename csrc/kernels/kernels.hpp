@@ -96,12 +96,12 @@ enum MaskMode : int { kMaskNone = 0, kMaskFull = 1, kMaskChaCha = 2 };
 // representatives) fused with masking and per-tile varint byte counts.
 //   secrets  [P][D] int32 ; shares [n][P][D] (u16 if value_bytes==2 else u32)
 //   cnt      [n][P][T] tile byte counts (T = ceil(D / kTileValues))
-//   mask_out [P][D] u32 (kMaskFull) and mask_cnt [P][T]
-//   seeds    [P][seed_words] u32 (kMaskChaCha, produced here from the CSPRNG)
+//   mask_out [P][D] (kMaskFull; the same element type as `shares`) and mask_cnt [P][T]
+// mask_mode is kMaskNone or kMaskFull; ChaCha-masked participants mask first
+// (launch_chacha_mask_apply) and share the masked vectors with kMaskNone.
 void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, const int32_t* secrets,
-                           int mask_mode, int seed_words, RngKeyArg rng, uint64_t owner_base,
-                           void* shares, uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt,
-                           uint32_t* seeds, uint32_t* err, hipStream_t s);
+                           int mask_mode, RngKeyArg rng, uint64_t owner_base, void* shares,
+                           uint32_t* cnt, void* mask_out, uint32_t* mask_cnt, hipStream_t s);
 
 // Additive share kernel selection -- benchmarking switch: 1 (default) = three
 // draws per word where m^3 < 2^32, else 16-bit halves; 2 = 16-bit halves; 0 = u32.
@@ -114,17 +114,35 @@ void set_pss48(int mode);
 // host-computed from the tss FFT construction).
 void launch_share_pss(int P, int D, int n, int k, int t, uint32_t p, int value_bytes,
                       const int32_t* secrets, const uint32_t* share_matrix, int mask_mode,
-                      int seed_words, RngKeyArg rng, uint64_t owner_base, void* shares,
-                      uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt, uint32_t* seeds,
-                      uint32_t* err, hipStream_t s);
+                      RngKeyArg rng, uint64_t owner_base, void* shares, uint32_t* cnt,
+                      void* mask_out, uint32_t* mask_cnt, hipStream_t s);
 
 // Tile byte counts for arbitrary canonical value vectors [M][L].
 void launch_count(int M, int L, int value_bytes, const void* vals, uint32_t* cnt, hipStream_t s);
 
-// rand-0.3 ChaChaRng mask expansion summed over participants:
-//   out[e] = sum_p gen_range(0, m)_e(seed_p) mod m      (chacha.rs:56-77)
+// ---- chacha_mask.hip -------------------------------------------------------
+// ChaCha masks (client/src/crypto/masking/chacha.rs): rand-0.3 ChaChaRng streams,
+// exact under rejected draws (a rejection shifts the rest of that participant's
+// stream; fast kernels record it, gated repair kernels re-index the stream).
+// seeds [P][seed_words] u32 from the round's CSPRNG:
+void launch_chacha_seeds(int P, int seed_words, RngKeyArg rng, uint64_t owner_base, uint32_t* seeds,
+                         hipStream_t s);
+// u32 words of `scratch` both launches below need (contents need no initialisation)
+size_t chacha_scratch_words(int P, int D);
+// participants: masked[p][e] = (secrets[p][e] + gen_range(0, m)_e(seed_p)) mod m
+void launch_chacha_mask_apply(int P, int D, uint32_t m, int seed_words, const uint32_t* seeds,
+                              const int32_t* secrets, int32_t* masked, uint32_t* scratch,
+                              uint32_t* err, hipStream_t s);
+// recipient: out[e] = sum_p gen_range(0, m)_e(seed_p) mod m      (chacha.rs:56-77).
+// part [groups][D] u32 slabs (groups = chacha_sum_groups(P, D)), fix [D] u64.
+int chacha_sum_groups(int P, int D);
 void launch_chacha_mask_sum(int P, int D, uint32_t m, int seed_words, const uint32_t* seeds,
-                            uint32_t* out, uint32_t* err, hipStream_t s);
+                            uint32_t* out, uint32_t* part, int groups, uint32_t* scratch,
+                            uint64_t* fix, uint32_t* err, hipStream_t s);
+// Test hook: cap the rand-0.3 acceptance zone (draws at or above cap - cap % m are
+// rejected) so that rejections, 1e-10 per draw at most in production, can be made
+// frequent. ~0 = no cap. The host model has the same hook (crypto.hpp).
+void set_chacha_zone_cap(uint64_t cap);
 
 // ---- seal.hip --------------------------------------------------------------
 // Segmented exclusive scan of rows [M][T] in place; totals[M] = row sums. With

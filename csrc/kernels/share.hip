@@ -85,54 +85,10 @@ SDA_DEV void load16_secrets(uint32_t (&x)[16], const int32_t* src, int valid, bo
   }
 }
 
-// rand-0.3 ChaChaRng block `ctr` (128-bit counter, here < 2^64) for a seed.
-SDA_DEV void chacharng_block(uint32_t (&w)[16], const uint32_t (&key)[8], uint64_t ctr) {
-  uint32_t in[16] = {kSigma0, kSigma1, kSigma2, kSigma3, key[0], key[1], key[2], key[3],
-                     key[4],  key[5],  key[6],  key[7],  (uint32_t)ctr, (uint32_t)(ctr >> 32), 0, 0};
-  chacha_block<20>(w, in);
-}
-
-// ChaCha mask for 16 consecutive elements starting at e0 (e0 % 8 == 0).
-SDA_DEV void chacha_mask16(uint32_t (&mk)[16], const uint32_t (&key)[8], uint64_t e0,
-                           const ModParams& mp, uint32_t* err) {
-  bool rej = false;
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    uint32_t w[16];
-    chacharng_block(w, key, e0 / 8 + half);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint64_t v = ((uint64_t)w[2 * i] << 32) | w[2 * i + 1];
-      rej |= v >= mp.zone64;
-      mk[8 * half + i] = mod64(v, mp);
-    }
-  }
-  if (rej) atomicOr(err, kErrChaChaReject);
-}
-
-// `p` is wave-uniform at every call site: keep the key in SGPRs.
-SDA_DEV void load_seed_key(uint32_t (&key)[8], const uint32_t* seeds, int p, int seed_words) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    key[i] = __builtin_amdgcn_readfirstlane(i < seed_words ? seeds[(size_t)p * seed_words + i] : 0u);
-}
-
 SDA_DEV uint32_t draw(uint32_t w, const RngKey& rk, uint64_t retry_purpose, uint64_t owner,
                       uint64_t idx, const ModParams& mp) {
   if ((uint64_t)w < mp.zone32) return mod32(w, mp);
   return uniform_fixup(rk, retry_purpose, owner, idx, mp.m, (uint32_t)mp.zone32);
-}
-
-__global__ void k_chacha_seeds(int P, int seed_words, RngKeyArg rng, uint64_t owner_base,
-                               uint32_t* seeds) {
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
-  RngKey rk = to_key(rng);
-  uint32_t w[16];
-  rng_block(w, rk, stream_id(kPurposeChaChaSeed, owner_base + p), 0);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if (i < seed_words) seeds[(size_t)p * seed_words + i] = w[i];
 }
 
 // ------------------------------------------------------------- additive ----
@@ -164,9 +120,8 @@ template <typename VT, int MASK>
 __global__ void __launch_bounds__(kBlock)
     k_share_additive(int P, int D, int n, ModParams mp, const int32_t* __restrict__ secrets,
                      RngKeyArg rng, uint64_t owner_base, VT* __restrict__ shares,
-                     uint32_t* __restrict__ cnt, uint32_t* __restrict__ mask_out,
-                     uint32_t* __restrict__ mask_cnt, const uint32_t* __restrict__ seeds,
-                     int seed_words, uint32_t* err) {
+                     uint32_t* __restrict__ cnt, VT* __restrict__ mask_out,
+                     uint32_t* __restrict__ mask_cnt) {
   __shared__ uint32_t partial[kMaxCountSlots + 1][kWaves];
   const int t = blockIdx.x, p = blockIdx.y, T = gridDim.x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -191,15 +146,9 @@ __global__ void __launch_bounds__(kBlock)
       last[i] = add_mod(last[i], w[i], m);
       bytes += i < valid ? vlen(w[i]) : 0u;
     }
-    store16<uint32_t>(mask_out + (size_t)p * D + e0, w, valid, vec_ok);
+    store16<VT>(mask_out + (size_t)p * D + e0, w, valid, vec_ok);
     bytes = wave_sum(bytes);
     if (lane == 0) partial[kMaxCountSlots][wave] = bytes;
-  } else if constexpr (MASK == kMaskChaCha) {
-    uint32_t key[8], mk[16];
-    load_seed_key(key, seeds, p, seed_words);
-    chacha_mask16(mk, key, (uint64_t)e0, mp, err);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) last[i] = add_mod(last[i], mk[i], m);
   }
 
   const int w_draws = n - 1;
@@ -264,7 +213,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     k_share_additive16(int P, int D, int n, ModParams mp, uint32_t zone16,
                        const int32_t* __restrict__ secrets, RngKeyArg rng, uint64_t owner_base,
                        uint16_t* __restrict__ shares, uint32_t* __restrict__ cnt,
-                       uint32_t* __restrict__ mask_out, uint32_t* __restrict__ mask_cnt) {
+                       uint16_t* __restrict__ mask_out, uint32_t* __restrict__ mask_cnt) {
   // partial[row][group][wave] byte counts; the final share at index kMaxRows16
   __shared__ uint32_t partial[kMaxRows16 + 1][kG16][kWaves];
   const int blk = blockIdx.x, p = blockIdx.y;
@@ -332,7 +281,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
           bytes += i < valid ? vlen(v[i]) : 0u;
         }
         if (is_mask) {
-          store16<uint32_t>(mask_out + (size_t)p * D + e0, v, valid, vec_ok);
+          store16<uint16_t>(mask_out + (size_t)p * D + e0, v, valid, vec_ok);
         } else {
           store16<uint16_t>(shares + ((size_t)(row - kMaskRows) * P + p) * D + e0, v, valid,
                             vec_ok);
@@ -427,7 +376,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     k_share_additive16p(int P, int D, int n, ModParams mp, uint32_t zone16,
                         const int32_t* __restrict__ secrets, RngKeyArg rng, uint64_t owner_base,
                         uint16_t* __restrict__ shares, uint32_t* __restrict__ cnt,
-                        uint32_t* __restrict__ mask_out, uint32_t* __restrict__ mask_cnt) {
+                        uint16_t* __restrict__ mask_out, uint32_t* __restrict__ mask_cnt) {
   __shared__ uint32_t partial[kMaxRows16 + 1][kGP][kWaves];
   const int blk = blockIdx.x, p = blockIdx.y;
   const int T = (D + kTileValues - 1) / kTileValues;
@@ -514,7 +463,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
           uint32_t v[16];
 #pragma unroll
           for (int k = 0; k < 8; ++k) { v[2 * k] = vp[k] & 0xffffu; v[2 * k + 1] = vp[k] >> 16; }
-          store16<uint32_t>(mask_out + (size_t)p * D + e0, v, valid, vec_ok);
+          store16<uint16_t>(mask_out + (size_t)p * D + e0, v, valid, vec_ok);
         } else {
           store_pairs(shares + ((size_t)(row - kMaskRows) * P + p) * D + e0, vp, valid, vec_ok);
         }
@@ -578,7 +527,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
     k_share_additive48(int P, int D, int n, ModParams mp, uint32_t m3, uint32_t t3,
                        const int32_t* __restrict__ secrets, RngKeyArg rng, uint64_t owner_base,
                        uint16_t* __restrict__ shares, uint32_t* __restrict__ cnt,
-                       uint32_t* __restrict__ mask_out, uint32_t* __restrict__ mask_cnt) {
+                       uint16_t* __restrict__ mask_out, uint32_t* __restrict__ mask_cnt) {
   __shared__ uint32_t partial[kMaxRows16 + 1][3 * kT3][kWaves];
   const int blk = blockIdx.x, p = blockIdx.y;
   const int T = (D + kTileValues - 1) / kTileValues;
@@ -662,7 +611,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
           uint32_t v[16];
 #pragma unroll
           for (int k = 0; k < 8; ++k) { v[2 * k] = vp[k] & 0xffffu; v[2 * k + 1] = vp[k] >> 16; }
-          store16<uint32_t>(mask_out + (size_t)p * D + e0[c], v, valid[c], vec_ok);
+          store16<uint16_t>(mask_out + (size_t)p * D + e0[c], v, valid[c], vec_ok);
         } else {
           store_pairs(shares + ((size_t)(r - kMaskRows) * P + p) * D + e0[c], vp, valid[c], vec_ok);
         }
@@ -715,9 +664,8 @@ __global__ void __launch_bounds__(kBlock)
     k_share_pss(int P, int D, int n, int k, int t, ModParams mp, int small_acc,
                 const int32_t* __restrict__ secrets, const uint32_t* __restrict__ mat,
                 RngKeyArg rng, uint64_t owner_base, VT* __restrict__ shares,
-                uint32_t* __restrict__ cnt, uint32_t* __restrict__ mask_out,
-                uint32_t* __restrict__ mask_cnt, const uint32_t* __restrict__ seeds,
-                int seed_words, uint32_t* err) {
+                uint32_t* __restrict__ cnt, VT* __restrict__ mask_out,
+                uint32_t* __restrict__ mask_cnt) {
   __shared__ uint32_t sM[kPssMaxN * (kPssMaxK + kPssMaxT)];
   __shared__ uint32_t scratch[kWaves];
   const int K = k + t;
@@ -731,8 +679,6 @@ __global__ void __launch_bounds__(kBlock)
   const uint32_t m = mp.m;
 
   uint32_t mask_bytes = 0;
-  uint32_t seedkey[8];
-  if constexpr (MASK == kMaskChaCha) load_seed_key(seedkey, seeds, p, seed_words);
 
   // per-clerk byte counters live in LDS-free registers only for small n; use
   // one pass per clerk group of 8 to bound registers.
@@ -755,16 +701,9 @@ __global__ void __launch_bounds__(kBlock)
               uint32_t mk = draw(w[e % 16], rk, kPurposeMaskRetry, owner, (uint64_t)e, mp);
               x = add_mod(x, mk, m);
               if (cg == 0) {
-                mask_out[(size_t)p * D + e] = mk;
+                mask_out[(size_t)p * D + e] = (VT)mk;
                 mask_bytes += vlen(mk);
               }
-            } else if constexpr (MASK == kMaskChaCha) {
-              uint32_t w[16];
-              chacharng_block(w, seedkey, (uint64_t)e / 8);
-              const int q = (e % 8) * 2;
-              uint64_t vv = ((uint64_t)w[q] << 32) | w[q + 1];
-              if (vv >= mp.zone64) atomicOr(err, kErrChaChaReject);
-              x = add_mod(x, mod64(vv, mp), m);
             }
           }
           v[j] = x;
@@ -1032,35 +971,6 @@ __global__ void __launch_bounds__(kBlock) k_count(int L, const VT* __restrict__ 
   if (threadIdx.x == 0) cnt[(size_t)j * T + t] = tot;
 }
 
-// ---------------------------------------------------- ChaCha mask (recipient)
-// out[e] = sum_p mask_p[e] mod m; each lane expands 8 elements (one ChaCha block)
-// of every participant's stream.
-__global__ void __launch_bounds__(kBlock)
-    k_chacha_mask_sum(int P, int D, ModParams mp, int seed_words,
-                      const uint32_t* __restrict__ seeds, uint32_t* __restrict__ out,
-                      uint32_t* err) {
-  const int e0 = (blockIdx.x * kBlock + threadIdx.x) * 8;
-  if (e0 >= D) return;
-  uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  bool rej = false;
-  for (int p = 0; p < P; ++p) {
-    uint32_t key[8];
-    load_seed_key(key, seeds, p, seed_words);
-    uint32_t w[16];
-    chacharng_block(w, key, (uint64_t)e0 / 8);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint64_t v = ((uint64_t)w[2 * i] << 32) | w[2 * i + 1];
-      rej |= v >= mp.zone64;
-      acc[i] = add_mod(acc[i], mod64(v, mp), mp.m);
-    }
-  }
-  if (rej) atomicOr(err, kErrChaChaReject);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if (e0 + i < D) out[e0 + i] = acc[i];
-}
-
 }  // namespace
 
 static int g_share16 = 1;
@@ -1069,19 +979,16 @@ static int g_pss48 = 1;
 void set_pss48(int mode) { g_pss48 = mode; }
 
 void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, const int32_t* secrets,
-                           int mask_mode, int seed_words, RngKeyArg rng, uint64_t owner_base,
-                           void* shares, uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt,
-                           uint32_t* seeds, uint32_t* err, hipStream_t s) {
+                           int mask_mode, RngKeyArg rng, uint64_t owner_base, void* shares,
+                           uint32_t* cnt, void* mask_out, uint32_t* mask_cnt, hipStream_t s) {
   if (P <= 0 || D <= 0) return;
   if (n < 1 || n > kMaxCountSlots) return;  // rejected by the binding (n == 1: masking only)
+  if (mask_mode != kMaskNone && mask_mode != kMaskFull) return;  // ChaCha masks: launch_chacha_mask_apply
   ModParams mp = make_mod_params(m);
-  if (mask_mode == kMaskChaCha)
-    hipLaunchKernelGGL(k_chacha_seeds, dim3((P + 63) / 64), dim3(64), 0, s, P, seed_words, rng,
-                       owner_base, seeds);
   // 16-bit draws: u16 shares, no ChaCha mask, room for the rows in LDS
   const bool rows_ok = (n - 1) + (mask_mode == kMaskFull ? 1 : 0) <= kMaxRows16;
   const uint64_t m3 = (uint64_t)m * m * m;
-  if (g_share16 == 1 && value_bytes == 2 && m3 < (1ull << 32) && mask_mode != kMaskChaCha && rows_ok) {
+  if (g_share16 == 1 && value_bytes == 2 && m3 < (1ull << 32) && rows_ok) {
     const uint32_t t3 = (uint32_t)((1ull << 32) % m3);  // reject x with lo(x m^3) < t3
     // six triples per block amortise the lanes' spare ChaCha block better (2.50 -> 2.43 ms
     // at 1000 x 1M); small launches (participant waves) keep three for twice the blocks
@@ -1092,15 +999,15 @@ void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, con
                     ? (t3n == 6 ? k_share_additive48<kMaskFull, 6> : k_share_additive48<kMaskFull, 3>)
                     : (t3n == 6 ? k_share_additive48<kMaskNone, 6> : k_share_additive48<kMaskNone, 3>);
     hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, P, D, n, mp, (uint32_t)m3, t3, secrets, rng,
-                       owner_base, (uint16_t*)shares, cnt, mask_out, mask_cnt);
+                       owner_base, (uint16_t*)shares, cnt, (uint16_t*)mask_out, mask_cnt);
     return;
   }
-  if (g_share16 && value_bytes == 2 && m <= 32768u && mask_mode != kMaskChaCha && rows_ok) {
+  if (g_share16 && value_bytes == 2 && m <= 32768u && rows_ok) {
     const uint32_t zone16 = 65536u - (65536u % m);
     dim3 grid((D + kGP * kTileValues - 1) / (kGP * kTileValues), P);
 #define SDA_P16(MK, SH)                                                                      \
   hipLaunchKernelGGL((k_share_additive16p<MK, SH>), grid, dim3(kBlock), 0, s, P, D, n, mp, zone16, \
-                     secrets, rng, owner_base, (uint16_t*)shares, cnt, mask_out, mask_cnt)
+                     secrets, rng, owner_base, (uint16_t*)shares, cnt, (uint16_t*)mask_out, mask_cnt)
     if (mask_mode == kMaskFull) {
       if (m <= 8192u) SDA_P16(kMaskFull, true); else SDA_P16(kMaskFull, false);
     } else {
@@ -1109,31 +1016,28 @@ void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, con
 #undef SDA_P16
     return;
   }
-  if (g_share16 && value_bytes == 2 && m < 65536u && mask_mode != kMaskChaCha && rows_ok) {
+  if (g_share16 && value_bytes == 2 && m < 65536u && rows_ok) {
     const uint32_t zone16 = 65536u - (65536u % m);
     dim3 grid16((D + kG16 * kTileValues - 1) / (kG16 * kTileValues), P);
     if (mask_mode == kMaskFull)
       hipLaunchKernelGGL(k_share_additive16<kMaskFull>, grid16, dim3(kBlock), 0, s, P, D, n, mp,
-                         zone16, secrets, rng, owner_base, (uint16_t*)shares, cnt, mask_out,
-                         mask_cnt);
+                         zone16, secrets, rng, owner_base, (uint16_t*)shares, cnt,
+                         (uint16_t*)mask_out, mask_cnt);
     else
       hipLaunchKernelGGL(k_share_additive16<kMaskNone>, grid16, dim3(kBlock), 0, s, P, D, n, mp,
-                         zone16, secrets, rng, owner_base, (uint16_t*)shares, cnt, mask_out,
-                         mask_cnt);
+                         zone16, secrets, rng, owner_base, (uint16_t*)shares, cnt,
+                         (uint16_t*)mask_out, mask_cnt);
     return;
   }
   dim3 grid((D + kTileValues - 1) / kTileValues, P);
 #define SDA_ADD_LAUNCH(VT, MK)                                                                \
   hipLaunchKernelGGL((k_share_additive<VT, MK>), grid, dim3(kBlock), 0, s, P, D, n, mp,        \
-                     secrets, rng, owner_base, (VT*)shares, cnt, mask_out, mask_cnt, seeds,    \
-                     seed_words, err)
+                     secrets, rng, owner_base, (VT*)shares, cnt, (VT*)mask_out, mask_cnt)
   if (value_bytes == 2) {
     if (mask_mode == kMaskFull) SDA_ADD_LAUNCH(uint16_t, kMaskFull);
-    else if (mask_mode == kMaskChaCha) SDA_ADD_LAUNCH(uint16_t, kMaskChaCha);
     else SDA_ADD_LAUNCH(uint16_t, kMaskNone);
   } else {
     if (mask_mode == kMaskFull) SDA_ADD_LAUNCH(uint32_t, kMaskFull);
-    else if (mask_mode == kMaskChaCha) SDA_ADD_LAUNCH(uint32_t, kMaskChaCha);
     else SDA_ADD_LAUNCH(uint32_t, kMaskNone);
   }
 #undef SDA_ADD_LAUNCH
@@ -1141,18 +1045,15 @@ void launch_share_additive(int P, int D, int n, uint32_t m, int value_bytes, con
 
 void launch_share_pss(int P, int D, int n, int k, int t, uint32_t p, int value_bytes,
                       const int32_t* secrets, const uint32_t* share_matrix, int mask_mode,
-                      int seed_words, RngKeyArg rng, uint64_t owner_base, void* shares,
-                      uint32_t* cnt, uint32_t* mask_out, uint32_t* mask_cnt, uint32_t* seeds,
-                      uint32_t* err, hipStream_t s) {
+                      RngKeyArg rng, uint64_t owner_base, void* shares, uint32_t* cnt,
+                      void* mask_out, uint32_t* mask_cnt, hipStream_t s) {
   if (P <= 0 || D <= 0) return;
+  if (mask_mode != kMaskNone && mask_mode != kMaskFull) return;  // ChaCha masks: launch_chacha_mask_apply
   ModParams mp = make_mod_params(p);
   const int B = (D + k - 1) / k;
   // accumulate in u64 without intermediate reduction when K*(p-1)^2 < 2^64
   const double bound = (double)(k + t) * (double)(p - 1) * (double)(p - 1);
   const int small_acc = bound < 1.8e19 ? 1 : 0;
-  if (mask_mode == kMaskChaCha)
-    hipLaunchKernelGGL(k_chacha_seeds, dim3((P + 63) / 64), dim3(64), 0, s, P, seed_words, rng,
-                       owner_base, seeds);
   dim3 grid((B + kTileValues - 1) / kTileValues, P);
   const uint64_t p3 = (uint64_t)p * p * p;
   if (g_pss48 && value_bytes <= 2 && mask_mode == kMaskNone && k == kPssKS && n == kPssNC &&
@@ -1182,18 +1083,15 @@ void launch_share_pss(int P, int D, int n, int k, int t, uint32_t p, int value_b
 #define SDA_PSS_LAUNCH(VT, MK)                                                             \
   hipLaunchKernelGGL((k_share_pss<VT, MK>), grid, dim3(kBlock), 0, s, P, D, n, k, t, mp,       \
                      small_acc, secrets, share_matrix, rng, owner_base, (VT*)shares, cnt,      \
-                     mask_out, mask_cnt, seeds, seed_words, err)
+                     (VT*)mask_out, mask_cnt)
   if (value_bytes == 1) {
     if (mask_mode == kMaskFull) SDA_PSS_LAUNCH(uint8_t, kMaskFull);
-    else if (mask_mode == kMaskChaCha) SDA_PSS_LAUNCH(uint8_t, kMaskChaCha);
     else SDA_PSS_LAUNCH(uint8_t, kMaskNone);
   } else if (value_bytes == 2) {
     if (mask_mode == kMaskFull) SDA_PSS_LAUNCH(uint16_t, kMaskFull);
-    else if (mask_mode == kMaskChaCha) SDA_PSS_LAUNCH(uint16_t, kMaskChaCha);
     else SDA_PSS_LAUNCH(uint16_t, kMaskNone);
   } else {
     if (mask_mode == kMaskFull) SDA_PSS_LAUNCH(uint32_t, kMaskFull);
-    else if (mask_mode == kMaskChaCha) SDA_PSS_LAUNCH(uint32_t, kMaskChaCha);
     else SDA_PSS_LAUNCH(uint32_t, kMaskNone);
   }
 #undef SDA_PSS_LAUNCH
@@ -1208,15 +1106,6 @@ void launch_count(int M, int L, int value_bytes, const void* vals, uint32_t* cnt
     hipLaunchKernelGGL(k_count<uint16_t>, grid, dim3(kBlock), 0, s, L, (const uint16_t*)vals, cnt);
   else
     hipLaunchKernelGGL(k_count<uint32_t>, grid, dim3(kBlock), 0, s, L, (const uint32_t*)vals, cnt);
-}
-
-void launch_chacha_mask_sum(int P, int D, uint32_t m, int seed_words, const uint32_t* seeds,
-                            uint32_t* out, uint32_t* err, hipStream_t s) {
-  if (D <= 0) return;
-  ModParams mp = make_mod_params(m);
-  int threads = (D + 7) / 8;
-  hipLaunchKernelGGL(k_chacha_mask_sum, dim3((threads + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                     P, D, mp, seed_words, seeds, out, err);
 }
 
 }  // namespace sdagpu

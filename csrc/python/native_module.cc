@@ -84,6 +84,8 @@ PYBIND11_MODULE(_sda_native, m) {
     crypto::chacha20_block_words(out, in.data(), rounds);
     return std::vector<uint32_t>(out, out + 16);
   }, py::arg("words"), py::arg("rounds") = 20);
+  c.def("set_chacha_zone_cap", &crypto::set_chacha_zone_cap,
+        "test hook: cap the rand-0.3 acceptance zone of ChaChaRng.gen_range (2^64 - 1 = none)");
   py::class_<crypto::ChaChaRng>(c, "ChaChaRng")
       .def(py::init([](std::vector<uint32_t> seed) {
         return new crypto::ChaChaRng(seed.data(), seed.size());

@@ -5,6 +5,7 @@
 // (reference client/src/crypto/encryption/sodium.rs:43,78). ChaChaRng reproduces
 // `rand::ChaChaRng::from_seed` + `gen_range(0, m)` used by the ChaCha mask
 // (client/src/crypto/masking/chacha.rs:29-39,67-72).
+#include <atomic>
 #include <cstring>
 
 #include "sda/crypto.hpp"
@@ -144,10 +145,17 @@ uint64_t ChaChaRng::next_u64() {
   uint64_t lo = next_u32();
   return (hi << 32) | lo;
 }
+namespace {
+std::atomic<uint64_t> g_zone_cap{UINT64_MAX};
+}
+void set_chacha_zone_cap(uint64_t cap) { g_zone_cap.store(cap); }
+
 int64_t ChaChaRng::gen_range(int64_t low, int64_t high) {
   if (!(low < high)) throw SdaError("gen_range: empty range");
   uint64_t range = (uint64_t)high - (uint64_t)low;
   uint64_t zone = UINT64_MAX - UINT64_MAX % range;
+  const uint64_t cap = g_zone_cap.load(std::memory_order_relaxed);
+  if (cap != UINT64_MAX && cap - cap % range < zone) zone = cap - cap % range;  // test hook
   for (;;) {
     uint64_t v = next_u64();
     if (v < zone) return (int64_t)((uint64_t)low + v % range);

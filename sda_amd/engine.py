@@ -200,42 +200,39 @@ class DeviceAggregator:
         dev = self.device
         shares = torch.empty(n, P, B, dtype=self.vdtype, device=dev)
         cnt = torch.empty(n * P * G.tiles(B), dtype=torch.int32, device=dev)
-        mask_mode, mask_vals, mask_cnt, seed_words = G.MASK_NONE, None, None, 0
-        if isinstance(spec.masking, FullMask):
-            mask_mode = G.MASK_FULL
-            mask_vals = torch.empty(P, D, dtype=torch.int32, device=dev)
+        mask_vals, mask_cnt = None, None
+        full = isinstance(spec.masking, FullMask)
+        if isinstance(spec.masking, ChaChaMask):
+            # masking/chacha.rs:29-45: a fresh seed per participant, masked = secret +
+            # its rand-0.3 stream. A pre-pass, so the shares come from the fast kernels;
+            # what travels to the recipient is the seed.
+            mask_vals = G.chacha_seeds(P, spec.masking.seed_words, rng_key, owner_base, dev)
+            secrets = G.chacha_mask_apply(secrets, mask_vals, m, err)
+        elif full:
+            # the masks in the shares' storage type (u16 where m <= 65536: half the
+            # bytes written here and read by the encoder), 32-bit ahead of the limb GEMM
+            mask_vals = torch.empty(P, D, dtype=torch.int32 if self._pss_mfma else self.vdtype,
+                                    device=dev)
             mask_cnt = torch.empty(P * G.tiles(D), dtype=torch.int32, device=dev)
-        elif isinstance(spec.masking, ChaChaMask):
-            mask_mode = G.MASK_CHACHA
-            seed_words = spec.masking.seed_words
-            mask_vals = torch.empty(P, seed_words, dtype=torch.int32, device=dev)
         if self._pss_mfma:
             # masks (if any) first, then S = M . X on the matrix cores
             masked = secrets
-            if mask_mode != G.MASK_NONE:
-                masked = G.mask_secrets(secrets, m, mask_mode, rng_key, owner_base,
-                                        mask_out=mask_vals if mask_mode == G.MASK_FULL else None,
-                                        mask_cnt=mask_cnt,
-                                        seeds=mask_vals if mask_mode == G.MASK_CHACHA else None,
-                                        seed_words=seed_words, err=err)
+            if full:
+                masked = G.mask_secrets(secrets, m, rng_key, owner_base, mask_vals, mask_cnt)
             ps = spec.sharing
             X = G.pss_x_limbs(masked, ps.secret_count, ps.privacy_threshold_, m, rng_key, owner_base)
             G.modgemm_i8(self._M_limbs, X, m, shares, ldc_z=B, ldc_m=P * B, ldc_n=1,
                          limit=n * P * B)
             return shares, None, mask_vals, mask_cnt
+        mode = G.MASK_FULL if full else G.MASK_NONE
         if self._pss is None:
-            G.share_additive(secrets, n, m, shares, cnt, mask_mode, rng_key, owner_base,
-                             mask_out=mask_vals if mask_mode == G.MASK_FULL else None,
-                             mask_cnt=mask_cnt,
-                             seeds=mask_vals if mask_mode == G.MASK_CHACHA else None,
-                             seed_words=seed_words, err=err)
+            G.share_additive(secrets, n, m, shares, cnt, mode, rng_key, owner_base,
+                             mask_out=mask_vals if full else None, mask_cnt=mask_cnt)
         else:
             ps = spec.sharing
             G.share_pss(secrets, n, ps.secret_count, ps.privacy_threshold_, m,
-                        self._share_matrix, shares, cnt, mask_mode, rng_key, owner_base,
-                        mask_out=mask_vals if mask_mode == G.MASK_FULL else None,
-                        seeds=mask_vals if mask_mode == G.MASK_CHACHA else None,
-                        seed_words=seed_words, err=err)
+                        self._share_matrix, shares, cnt, mode, rng_key, owner_base,
+                        mask_out=mask_vals if full else None)
             mask_cnt = None  # PSS batches do not align with mask tiles: recounted
         return shares, cnt, mask_vals, mask_cnt
 
@@ -624,7 +621,7 @@ def describe_error(e: int) -> str:
     if e & 4:
         names.append("malformed varint stream")
     if e & 8:
-        names.append("ChaCha mask rejection (host fallback needed)")
+        names.append("ChaCha mask stream: more than half of the draws rejected")
     if e & 16:
         names.append("value out of range")
     return ", ".join(names) or "none"

@@ -11,7 +11,7 @@ from dataclasses import dataclass
 from typing import Callable, Optional, Sequence
 
 from .schemes import (PSS_4_8_3, PSS_155_728_100, PSS_155_19682_100, Additive, AggregationSpec,
-                      NoMask, PackedShamir, pss_5_of_8)
+                      ChaChaMask, FullMask, NoMask, PackedShamir, pss_5_of_8)
 
 
 @dataclass(frozen=True)
@@ -26,11 +26,14 @@ class BenchConfig:
     wave: int = 32
     pss_backend: str = "auto"
     what: str = ""
+    masking: str = "none"          # none | full | chacha (client/src/crypto/masking/*.rs)
 
     def spec(self, dimension: Optional[int] = None) -> AggregationSpec:
         s = self.sharing()
-        return AggregationSpec(dimension or self.dimension, s.field_modulus, s, NoMask(),
-                               title=self.name)
+        D = dimension or self.dimension
+        mask = {"none": lambda: NoMask(), "full": lambda: FullMask(s.field_modulus),
+                "chacha": lambda: ChaChaMask(s.field_modulus, D)}[self.masking]()
+        return AggregationSpec(D, s.field_modulus, s, mask, title=self.name)
 
 
 def small_prime_5_of_8(prime: int = 241) -> PackedShamir:
@@ -73,6 +76,18 @@ BENCH_CONFIGS = {
                     pss_backend="mfma",
                     what="the reference's largest parameter set: 19,682 clerks, k=100, t=155 "
                          "(315k sealed boxes of 10,000 shares for 16 participants per GPU)"),
+        BenchConfig(9, "add3_fullmask_1kx1m", 1000, 1_000_000, lambda: Additive(3, 433),
+                    masking="full",
+                    what="headline shape with a full mask: every participant also seals its "
+                         "1M-value mask for the recipient, who opens and sums them"),
+        BenchConfig(10, "add3_chachamask_1kx1m", 1000, 1_000_000, lambda: Additive(3, 433),
+                    masking="chacha",
+                    what="headline shape with a ChaCha mask: participants expand a rand-0.3 "
+                         "ChaChaRng seed over the vector, the recipient re-expands all 1000 seeds"),
+        BenchConfig(11, "add3_chachamask_m31_1kx1m", 1000, 1_000_000,
+                    lambda: Additive(3, 2 ** 31 - 1), masking="chacha",
+                    what="ChaCha mask over the largest supported modulus (2^31 - 1): 32-bit "
+                         "shares, five-byte varints, a rejected draw every ~1e10"),
     ]
 }
 

@@ -136,56 +136,46 @@ def x25519(scalars: torch.Tensor, points: torch.Tensor) -> torch.Tensor:
 
 
 def share_additive(secrets, n, modulus, shares, cnt, mask_mode, rng_key, owner_base,
-                   mask_out=None, mask_cnt=None, seeds=None, seed_words=0, err=None):
+                   mask_out=None, mask_cnt=None):
+    """Additive shares of `secrets` [P][D] (+ a full mask with MASK_FULL). ChaCha-masked
+    participants mask first (:func:`chacha_mask_apply`) and share with MASK_NONE."""
     P, D = secrets.shape
     _check(secrets, "secrets", torch.int32)
     vb = value_bytes(shares.dtype)
     _check(shares, "shares", (torch.int16, torch.int32), numel=n * P * D)
     T = tiles(D)
     _check(cnt, "cnt", torch.int32, numel=n * P * T)
-    _check(err, "err", torch.int32, numel=1)
     if n < 2:
         raise ValueError("additive sharing needs at least 2 shares")
-    if mask_mode == MASK_FULL:
-        _check(mask_out, "mask_out", torch.int32, numel=P * D)
+    if mask_mode not in (MASK_NONE, MASK_FULL):
+        raise ValueError("share_additive: mask mode none or full")
+    if mask_mode == MASK_FULL:  # the masks are stored like the shares
+        _check(mask_out, "mask_out", shares.dtype, numel=P * D)
         _check(mask_cnt, "mask_cnt", torch.int32, numel=P * T)
-    if mask_mode == MASK_CHACHA:
-        if not 1 <= seed_words <= 8:
-            raise ValueError("seed_words must be 1..8")
-        _check(seeds, "seeds", torch.int32, numel=P * seed_words)
     z = 0
-    _gpu().share_additive(P, D, n, modulus, vb, _ptr(secrets), mask_mode, seed_words,
+    _gpu().share_additive(P, D, n, modulus, vb, _ptr(secrets), mask_mode,
                           rng_words(rng_key), owner_base, _ptr(shares), _ptr(cnt),
                           _ptr(mask_out) if mask_out is not None else z,
-                          _ptr(mask_cnt) if mask_cnt is not None else z,
-                          _ptr(seeds) if seeds is not None else z, _ptr(err), _stream())
+                          _ptr(mask_cnt) if mask_cnt is not None else z, _stream())
 
 
-def mask_secrets(secrets, modulus, mask_mode, rng_key, owner_base, mask_out=None, mask_cnt=None,
-                 seeds=None, seed_words=0, err=None) -> torch.Tensor:
-    """Masked secrets (canonical int32 [P][D]) + mask outputs: the additive
+def mask_secrets(secrets, modulus, rng_key, owner_base, mask_out, mask_cnt) -> torch.Tensor:
+    """Fully masked secrets (canonical int32 [P][D]) + the masks: the additive
     share kernel with a single share, whose only share is the masked secret."""
     P, D = secrets.shape
     _check(secrets, "secrets", torch.int32)
-    _check(err, "err", torch.int32, numel=1)
-    if mask_mode == MASK_FULL:
-        _check(mask_out, "mask_out", torch.int32, numel=P * D)
-        _check(mask_cnt, "mask_cnt", torch.int32, numel=P * tiles(D))
-    if mask_mode == MASK_CHACHA:
-        _check(seeds, "seeds", torch.int32, numel=P * seed_words)
+    _check(mask_out, "mask_out", torch.int32, numel=P * D)
+    _check(mask_cnt, "mask_cnt", torch.int32, numel=P * tiles(D))
     masked = torch.empty(P, D, dtype=torch.int32, device=secrets.device)
     cnt = torch.empty(P * tiles(D), dtype=torch.int32, device=secrets.device)
-    z = 0
-    _gpu().share_additive(P, D, 1, modulus, 4, _ptr(secrets), mask_mode, seed_words,
+    _gpu().share_additive(P, D, 1, modulus, 4, _ptr(secrets), MASK_FULL,
                           rng_words(rng_key), owner_base, _ptr(masked), _ptr(cnt),
-                          _ptr(mask_out) if mask_out is not None else z,
-                          _ptr(mask_cnt) if mask_cnt is not None else z,
-                          _ptr(seeds) if seeds is not None else z, _ptr(err), _stream())
+                          _ptr(mask_out), _ptr(mask_cnt), _stream())
     return masked
 
 
 def share_pss(secrets, n, k, t, prime, matrix, shares, cnt, mask_mode, rng_key, owner_base,
-              mask_out=None, seeds=None, seed_words=0, err=None):
+              mask_out=None):
     P, D = secrets.shape
     B = (D + k - 1) // k
     _check(secrets, "secrets", torch.int32)
@@ -195,16 +185,41 @@ def share_pss(secrets, n, k, t, prime, matrix, shares, cnt, mask_mode, rng_key, 
     if shares.dtype == torch.uint8 and prime > 256:
         raise ValueError("u8 share storage needs a prime <= 256")
     _check(cnt, "cnt", torch.int32, numel=n * P * tiles(B))
-    _check(err, "err", torch.int32, numel=1)
-    if mask_mode == MASK_FULL:
-        _check(mask_out, "mask_out", torch.int32, numel=P * D)
-    if mask_mode == MASK_CHACHA:
-        _check(seeds, "seeds", torch.int32, numel=P * seed_words)
+    if mask_mode not in (MASK_NONE, MASK_FULL):
+        raise ValueError("share_pss: mask mode none or full")
+    if mask_mode == MASK_FULL:  # the masks are stored like the shares
+        _check(mask_out, "mask_out", shares.dtype, numel=P * D)
     z = 0
-    _gpu().share_pss(P, D, n, k, t, prime, vb, _ptr(secrets), _ptr(matrix), mask_mode, seed_words,
+    _gpu().share_pss(P, D, n, k, t, prime, vb, _ptr(secrets), _ptr(matrix), mask_mode,
                      rng_words(rng_key), owner_base, _ptr(shares), _ptr(cnt),
-                     _ptr(mask_out) if mask_out is not None else z, z,
-                     _ptr(seeds) if seeds is not None else z, _ptr(err), _stream())
+                     _ptr(mask_out) if mask_out is not None else z, z, _stream())
+
+
+# ---- ChaCha masks (rand-0.3 ChaChaRng streams; chacha_mask.hip) ---------------------------
+def chacha_seeds(P: int, seed_words: int, rng_key: bytes, owner_base: int, device) -> torch.Tensor:
+    """Fresh per-participant mask seeds [P][seed_words] from the round's CSPRNG."""
+    if not 1 <= seed_words <= 8:
+        raise ValueError("seed_words must be 1..8")
+    seeds = torch.empty(P, seed_words, dtype=torch.int32, device=device)
+    _gpu().chacha_seeds(P, seed_words, rng_words(rng_key), owner_base, _ptr(seeds), _stream())
+    return seeds
+
+
+def chacha_mask_apply(secrets: torch.Tensor, seeds: torch.Tensor, modulus: int,
+                      err: torch.Tensor) -> torch.Tensor:
+    """masked[p][e] = (secrets[p][e] + mask_p[e]) mod m, mask_p = the rand-0.3
+    `gen_range(0, m)` stream of seed p (chacha.rs:29-45), exact under rejected draws."""
+    P, D = secrets.shape
+    _check(secrets, "secrets", torch.int32)
+    _check(seeds, "seeds", torch.int32)
+    if seeds.dim() != 2 or seeds.shape[0] != P or not 1 <= seeds.shape[1] <= 8:
+        raise ValueError("seeds must be [P][1..8] words")
+    _check(err, "err", torch.int32, numel=1)
+    masked = torch.empty_like(secrets)
+    scratch = torch.empty(_gpu().chacha_scratch_words(P, D), dtype=torch.int32, device=secrets.device)
+    _gpu().chacha_mask_apply(P, D, modulus, seeds.shape[1], _ptr(seeds), _ptr(secrets),
+                             _ptr(masked), _ptr(scratch), _ptr(err), _stream())
+    return masked
 
 
 def count(vals: torch.Tensor, cnt: torch.Tensor):
@@ -215,10 +230,19 @@ def count(vals: torch.Tensor, cnt: torch.Tensor):
 
 
 def chacha_mask_sum(seeds: torch.Tensor, D: int, modulus: int, out: torch.Tensor, err):
+    """out[e] = sum_p mask_p[e] mod m over the seeds [P][w] (chacha.rs:56-77), exact
+    under rejected draws."""
     P, w = seeds.shape
     _check(seeds, "seeds", torch.int32)
     _check(out, "out", torch.int32, numel=D)
-    _gpu().chacha_mask_sum(P, D, modulus, w, _ptr(seeds), _ptr(out), _ptr(err), _stream())
+    _check(err, "err", torch.int32, numel=1)
+    dev = seeds.device
+    groups = _gpu().chacha_sum_groups(P, D)
+    part = torch.empty(groups, D, dtype=torch.int32, device=dev)
+    scratch = torch.empty(_gpu().chacha_scratch_words(P, D), dtype=torch.int32, device=dev)
+    fix = torch.empty(D, dtype=torch.int64, device=dev)
+    _gpu().chacha_mask_sum(P, D, modulus, w, _ptr(seeds), _ptr(out), _ptr(part), groups,
+                           _ptr(scratch), _ptr(fix), _ptr(err), _stream())
 
 
 def segscan(data: torch.Tensor, totals: torch.Tensor | None, expect: int | None = None,

@@ -273,6 +273,106 @@ def test_chacha_mask_matches_rand03(cuda, native):
     assert int(err.item()) == 0
 
 
+class _zone_cap:
+    """rand-0.3 acceptance zone capped on the host model and the device kernels alike
+    (test hook): rejections, at most 1e-10 per draw in production, become frequent."""
+
+    def __init__(self, native, cap):
+        self.native, self.cap = native, cap
+
+    def __enter__(self):
+        from sda_amd._native import gpu
+        self.native.crypto.set_chacha_zone_cap(self.cap)
+        gpu().set_chacha_zone_cap(self.cap)
+
+    def __exit__(self, *exc):
+        from sda_amd._native import gpu
+        self.native.crypto.set_chacha_zone_cap(2 ** 64 - 1)
+        gpu().set_chacha_zone_cap(2 ** 64 - 1)
+
+
+def _host_masks(native, seeds, D, m):
+    out = []
+    for row in seeds.tolist():
+        rng = native.crypto.ChaChaRng([int(w) & 0xFFFFFFFF for w in row])
+        out.append([rng.gen_range(0, m) for _ in range(D)])
+    return torch.tensor(out, dtype=torch.int64)
+
+
+def _rejected_positions(native, seed_row, count, m, cap):
+    zone = min(2 ** 64 - 1 - (2 ** 64 - 1) % m, cap - cap % m)
+    rng = native.crypto.ChaChaRng([int(w) & 0xFFFFFFFF for w in seed_row])
+    return [d for d in range(count) if rng.next_u64() >= zone]
+
+
+@pytest.mark.parametrize("m,den", [(433, 16), (2 ** 31 - 1, 16), (433, 3)])
+def test_chacha_mask_with_rejected_draws_matches_rand03(cuda, native, m, den):
+    """rand 0.3 `gen_range` re-draws a rejected value, which shifts every later
+    element of that participant's stream (client/src/crypto/masking/chacha.rs:36-39,
+    67-72). With the acceptance zone capped so that about one draw in `den` is
+    rejected, the device expansion -- recipient sum and participant masking -- must
+    equal the host ChaChaRng element for element: rejections on a ChaCha block's
+    last draw, on a 2048-draw chunk's last draw, several in one block."""
+    from sda_amd.ops import gpu as G
+    P, D = 5, 6001  # three chunks of draws, a ragged tail
+    cap = 2 ** 64 - 2 ** 64 // den
+    g = torch.Generator().manual_seed(den * 7 + m % 97)
+    seeds = torch.randint(-2 ** 31, 2 ** 31, (P, 4), dtype=torch.int64, generator=g)
+    # participant 0's seed: a stream whose draw 2047 (last of the first chunk) is rejected
+    zone = cap - cap % m
+    for s0 in range(4000):
+        rng = native.crypto.ChaChaRng([s0])
+        for _ in range(2047):
+            rng.next_u64()
+        if rng.next_u64() >= zone:
+            seeds[0] = torch.tensor([s0, 0, 0, 0])
+            break
+    else:
+        pytest.fail("no seed with a rejection on a chunk's last draw")
+    seeds = seeds.to(torch.int32)
+    rej = [_rejected_positions(native, row, D + D // 2, m, cap) for row in seeds.tolist()]
+    assert 2047 in rej[0]
+    assert any(d % 8 == 7 for r in rej for d in r)                      # a block's last draw
+    assert any(a + 1 == b for r in rej for a, b in zip(r, r[1:]))       # two in a row
+    with _zone_cap(native, cap):
+        masks = _host_masks(native, seeds, D, m)
+        err = torch.zeros(1, dtype=torch.int32, device=cuda)
+        out = torch.empty(D, dtype=torch.int32, device=cuda)
+        G.chacha_mask_sum(seeds.to(cuda), D, m, out, err)
+        secrets = torch.randint(-m, m, (P, D), dtype=torch.int32, generator=g)
+        masked = G.chacha_mask_apply(secrets.to(cuda), seeds.to(cuda), m, err)
+        torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert torch.equal(out.cpu().to(torch.int64), masks.sum(0) % m)
+    assert torch.equal(masked.cpu().to(torch.int64), (secrets.to(torch.int64) + masks) % m)
+    # without the cap the same seeds expand without a rejection, to other values
+    out2 = torch.empty(D, dtype=torch.int32, device=cuda)
+    G.chacha_mask_sum(seeds.to(cuda), D, m, out2, err)
+    assert torch.equal(out2.cpu().to(torch.int64), _host_masks(native, seeds, D, m).sum(0) % m)
+    assert not torch.equal(out, out2)
+
+
+def test_chacha_mask_reports_a_stream_that_runs_dry(cuda, native):
+    """More than half of the draws rejected: the scanned range (2 D + 4096 draws)
+    cannot hold D accepted ones; the error word says so instead of a wrong sum."""
+    from sda_amd.ops import gpu as G
+    P, D, m = 2, 9000, 433
+    seeds = torch.tensor([[1, 2, 3, 4], [5, 6, 7, 8]], dtype=torch.int32, device=cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    out = torch.empty(D, dtype=torch.int32, device=cuda)
+    with _zone_cap(native, 2 ** 62):  # three draws in four rejected
+        G.chacha_mask_sum(seeds, D, m, out, err)
+        torch.cuda.synchronize()
+    assert int(err.item()) & 8
+
+
+def test_round_with_chacha_masks_under_rejections(cuda, native):
+    """A whole round whose participants and recipient both meet rejected draws."""
+    from sda_amd.models.schemes import Additive, AggregationSpec, ChaChaMask
+    with _zone_cap(native, 2 ** 64 - 2 ** 64 // 9):
+        _round(cuda, AggregationSpec(5003, 433, Additive(3, 433), ChaChaMask(433, 5003)), 7)
+
+
 def test_additive_shares_sum_to_secret(cuda):
     from sda_amd.ops import gpu as G
     P, D, n, m = 4, 5000, 3, 433
@@ -280,7 +380,7 @@ def test_additive_shares_sum_to_secret(cuda):
     shares = torch.empty(n, P, D, dtype=torch.int16, device=cuda)
     cnt = torch.empty(n * P * G.tiles(D), dtype=torch.int32, device=cuda)
     err = torch.zeros(1, dtype=torch.int32, device=cuda)
-    G.share_additive(secrets, n, m, shares, cnt, G.MASK_NONE, os.urandom(32), 0, err=err)
+    G.share_additive(secrets, n, m, shares, cnt, G.MASK_NONE, os.urandom(32), 0)
     s = shares.to(torch.int64).sum(0) % m
     assert torch.equal(s, torch.remainder(secrets.to(torch.int64), m))
     # random shares are spread over [0, m)

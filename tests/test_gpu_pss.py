@@ -22,7 +22,7 @@ def _shares(cuda, ps, secrets, switch=1):
     err = torch.zeros(1, dtype=torch.int32, device=cuda)
     gpu().set_pss48(switch)
     try:
-        G.share_pss(secrets, n, k, t, m, M, shares, cnt, G.MASK_NONE, bytes(range(32)), 0, err=err)
+        G.share_pss(secrets, n, k, t, m, M, shares, cnt, G.MASK_NONE, bytes(range(32)), 0)
         torch.cuda.synchronize()
     finally:
         gpu().set_pss48(1)

@@ -15,23 +15,24 @@ def _run(m, n, P, D, mask):
     shares = torch.empty(n, P, D, dtype=torch.int16, device="cuda")
     cnt = torch.empty(n * P * G.tiles(D), dtype=torch.int32, device="cuda")
     err = torch.zeros(1, dtype=torch.int32, device="cuda")
-    mask_out = torch.empty(P, D, dtype=torch.int32, device="cuda") if mask else None
+    mask_out = torch.empty(P, D, dtype=torch.int16, device="cuda") if mask else None
     mask_cnt = torch.empty(P * G.tiles(D), dtype=torch.int32, device="cuda") if mask else None
     G.share_additive(secrets, n, m, shares, cnt, G.MASK_FULL if mask else G.MASK_NONE,
-                     bytes(range(32)), 0, mask_out=mask_out, mask_cnt=mask_cnt, err=err)
+                     bytes(range(32)), 0, mask_out=mask_out, mask_cnt=mask_cnt)
     torch.cuda.synchronize()
     assert int(err.item()) == 0
     sh = shares.to(torch.int64) & 0xFFFF
     assert int(sh.max()) < m
     total = torch.remainder(sh.sum(0), m)
-    expect = torch.remainder(secrets.to(torch.int64) + (mask_out.to(torch.int64) if mask else 0), m)
+    expect = torch.remainder(secrets.to(torch.int64) + ((mask_out.to(torch.int64) & 0xFFFF) if mask else 0), m)
     assert torch.equal(total, expect)
     # tile byte counts equal a recount of the stored values
     recount = torch.empty_like(cnt)
     G.count(shares.view(n * P, D), recount)
     assert torch.equal(cnt, recount)
     if mask:
-        assert int(mask_out.max()) < m and int(mask_out.min()) >= 0
+        mv = mask_out.to(torch.int64) & 0xFFFF
+        assert int(mv.max()) < m and int(mv.min()) >= 0
         mrecount = torch.empty_like(mask_cnt)
         G.count(mask_out, mrecount)
         assert torch.equal(mask_cnt, mrecount)
