@@ -47,7 +47,10 @@ def parse():
     ap.add_argument("--pss-backend", default=None, choices=["auto", "valu", "mfma"])
     ap.add_argument("--participants", type=int, default=None, help="per rank")
     ap.add_argument("--dim", type=int, default=None)
-    ap.add_argument("--wave", type=int, default=None, help="participants per wave (config 4)")
+    ap.add_argument("--wave", type=int, default=None,
+                    help="participants per wave of a streamed configuration (default: what the "
+                         "HBM planner fits into the free device memory)")
+    ap.add_argument("--checkpoint-every", type=int, default=8, help="waves between checkpoints")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--layout", default="committee", choices=["committee", "owner"])
@@ -150,13 +153,16 @@ def gpu_configs(args):
         if world > 1:
             agg.comm.barrier()
 
+    free_at_start = eng.free_bytes()
+
     def gen(seed, count):
         g = torch.Generator(device=dev).manual_seed(seed)
         return torch.randint(0, m, (count, D), dtype=torch.int32, device=dev, generator=g)
 
     ok = None
+    stream_info = None
     if cfg.streamed:
-        wave = args.wave or cfg.wave
+        wave = args.wave  # None: the planner sizes the waves from the free HBM
         ck = (args.checkpoint + f".rank{rank}") if args.checkpoint else None
 
         def make(w, first, count):
@@ -164,13 +170,17 @@ def gpu_configs(args):
         sync()
         t0 = time.perf_counter()
         if world > 1:
-            res = agg.run_streamed(P, make, wave=wave, checkpoint=ck)
+            res = agg.run_streamed(P, make, wave=wave, checkpoint=ck,
+                                   checkpoint_every=args.checkpoint_every)
         else:
             from sda_amd.streaming import StreamingAggregator
 
-            res = StreamingAggregator(eng, wave=wave, checkpoint=ck).run(P, make)
+            res = StreamingAggregator(eng, wave=wave, checkpoint=ck,
+                                      checkpoint_every=args.checkpoint_every).run(P, make)
         sync()
         secs = time.perf_counter() - t0
+        wave = res.wave
+        stream_info = {"plan": res.plan, "checkpoint": res.checkpoint}
         if world > 1:
             secs = agg.comm.all_reduce_max(secs)
         if args.check:
@@ -230,7 +240,10 @@ def gpu_configs(args):
               "layout": args.layout if world > 1 else "single GPU",
               "hbm_high_water_bytes": torch.cuda.max_memory_allocated(),
               "hbm_reserved_bytes": torch.cuda.max_memory_reserved(),
-              "wave": (args.wave or cfg.wave) if cfg.streamed else None, "correct": ok})
+              "hbm_free_bytes_at_start": free_at_start,
+              "plan": (stream_info or {}).get("plan") if cfg.streamed else eng.plan(P).as_dict(),
+              "checkpoint": (stream_info or {}).get("checkpoint"),
+              "wave": wave if cfg.streamed else None, "correct": ok})
     if world > 1:
         dist.destroy_process_group()
 

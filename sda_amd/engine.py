@@ -274,6 +274,31 @@ class DeviceAggregator:
     def new_error_word(self) -> torch.Tensor:
         return torch.zeros(1, dtype=torch.int32, device=self.device)
 
+    # ------------------------------------------------------------- planning ----
+    def free_bytes(self) -> int:
+        """Device memory a round can still claim: what the driver reports free plus
+        what the caching allocator holds but has not handed out."""
+        free, _ = torch.cuda.mem_get_info(self.device)
+        held = torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
+        return int(free + max(0, held))
+
+    def plan(self, participants: int, input_resident: bool = True, free_bytes: int | None = None):
+        """The :class:`sda_amd.planner.RoundPlan` for `participants` vectors on this
+        device now (cached per participant count)."""
+        from .planner import plan_round
+
+        if free_bytes is None:
+            free_bytes = getattr(self, "memory_limit_bytes", None)  # a cap set by the caller
+        cache = self.__dict__.setdefault("_plans", {})
+        key = (participants, input_resident, free_bytes)
+        if key not in cache:
+            cache[key] = plan_round(
+                self.spec, participants, self.free_bytes() if free_bytes is None else free_bytes,
+                pss_backend="mfma" if self._pss_mfma else ("valu" if self._pss is not None else "auto"),
+                share_storage="u16" if self.vdtype == torch.int16 else "auto",
+                input_resident=input_resident)
+        return cache[key]
+
     def run_round(self, secrets: torch.Tensor, clerks: Sequence[int] | None = None,
                   check: bool = True, reducer=None, owner_base: int = 0) -> RoundResult:
         """One full round for participant vectors `secrets` [P][D] (int32, on device).
@@ -290,6 +315,16 @@ class DeviceAggregator:
         :class:`sda_amd.parallel.DistributedAggregator`'s ``committee`` layout.
         """
         live = self._live(clerks)
+        plan = self.plan(secrets.shape[0])
+        if not plan.resident:
+            # too large to be resident: the same round in participant waves (only the
+            # clerks' running sums persist between them) instead of an out-of-memory error
+            from .streaming import StreamingAggregator
+
+            st = StreamingAggregator(self, wave=plan.wave)
+            sr = st.run(secrets.shape[0], lambda w, first, count: secrets[first:first + count],
+                        clerks=clerks, reducer=reducer, owner_base=owner_base, check=check)
+            return RoundResult(sr.output, sr.clerks_used, sr.stage_ms, err=sr.err)
         err = self.new_error_word()
         marks: list = []
         self._mark(marks, "start")

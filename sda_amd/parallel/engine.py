@@ -214,18 +214,23 @@ class DistributedAggregator:
         out, used = cm.finish(ctx, acc, err, marks=marks)
         return eng._finish(err, marks, check, RoundResult(out, used, {}))
 
-    def run_streamed(self, total_local: int, make_wave, wave: int = 64,
+    def run_streamed(self, total_local: int, make_wave, wave: Optional[int] = None,
                      clerks: Optional[Sequence[int]] = None, checkpoint: Optional[str] = None,
                      checkpoint_every: int = 8, resume: bool = True):
         """Stream this rank's `total_local` participants in waves (device engine).
 
         Every rank must stream the same number of participants with the same
-        wave size. Checkpoints are per rank: pass a rank-specific path.
+        wave size (None: the smallest of the ranks' planned waves). Checkpoints are
+        per rank: pass a rank-specific path.
         """
         if self.kind != "device":
             raise ValueError("streaming runs on the device engine")
         from ..streaming import StreamingAggregator
 
+        if wave is None:
+            # every rank must cut its participants alike: agree on the smallest plan
+            mine = self.engine.plan(total_local, input_resident=False).wave
+            wave = max(1, int(-self.comm.all_reduce_max(-float(mine))))
         st = StreamingAggregator(self.engine, wave=wave, checkpoint=checkpoint,
                                  checkpoint_every=checkpoint_every)
         if self.layout == "owner":

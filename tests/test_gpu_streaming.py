@@ -57,3 +57,66 @@ def test_streamed_checkpoint_resume(cuda, tmp_path):
     other = StreamingAggregator(DeviceAggregator(spec, keys=eng.keys), wave=wave + 1, checkpoint=ck)
     with pytest.raises(AggregationError):
         other.run(total, make)
+
+
+def test_run_round_streams_when_the_round_does_not_fit(cuda):
+    """A round larger than the memory it may use runs in planner-sized waves
+    instead of failing: same output, and the plan says so."""
+    from sda_amd.engine import DeviceAggregator, reference_sum
+    from sda_amd.models import Additive, AggregationSpec, FullMask
+
+    m, D, P = 433, 50_000, 96
+    spec = AggregationSpec(D, m, Additive(3, m), FullMask(m))
+    agg = DeviceAggregator(spec)
+    x = torch.randint(0, m, (P, D), dtype=torch.int32, device="cuda")
+    assert agg.plan(P).resident
+    ref = reference_sum(x, m)
+    assert torch.equal(agg.run_round(x).output, ref)
+    small = DeviceAggregator(spec, keys=agg.keys)
+    small.memory_limit_bytes = 700 * 10 ** 6  # the slabs and sums alone are ~0.5 GB
+    plan = small.plan(P)
+    assert not plan.resident and 1 <= plan.wave < P, plan
+    res = small.run_round(x)
+    assert torch.equal(res.output, ref) and int(res.err.item()) == 0
+    with pytest.raises(MemoryError):
+        small.memory_limit_bytes = 10 ** 6
+        small.plan(P + 1)
+
+
+def test_planner_picks_the_wave_and_checkpoints_do_not_block(cuda, tmp_path):
+    from sda_amd.engine import DeviceAggregator
+    from sda_amd.models import PSS_4_8_3, AggregationSpec
+    from sda_amd.streaming import StreamingAggregator
+
+    m, D, total = 433, 30_000, 120
+    spec = AggregationSpec(D, m, PSS_4_8_3)
+    eng = DeviceAggregator(spec)
+    eng.memory_limit_bytes = 400 * 10 ** 6  # the fixed part is ~250 MB: room for ~50 participants
+    make = _waves(m, D, seed=3)
+    st = StreamingAggregator(eng, checkpoint=str(tmp_path / "ck.safetensors"), checkpoint_every=1)
+    res = st.run(total, make)
+    assert res.plan is not None and res.wave == res.plan["wave"] and 1 <= res.wave < total
+    assert res.waves == -(-total // res.wave)
+    assert torch.equal(res.output, _reference(make, total, res.wave, m))
+    # a checkpoint per wave was written by the background writer
+    assert res.checkpoint["written"] == res.waves
+    # resuming adopts the checkpoint's wave size even when the planner would pick another
+    eng2 = DeviceAggregator(spec, keys=eng.keys)
+    again = StreamingAggregator(eng2, checkpoint=str(tmp_path / "ck.safetensors")).run(total, make)
+    assert again.resumed_from == res.waves and again.waves == 0
+    assert torch.equal(again.output, res.output)
+
+
+def test_a_checkpoint_is_never_written_from_a_failed_wave(cuda, tmp_path):
+    from sda_amd.engine import AggregationError, DeviceAggregator
+    from sda_amd.models import Additive, AggregationSpec
+    from sda_amd.streaming import StreamingAggregator
+
+    spec = AggregationSpec(5000, 433, Additive(3, 433))
+    eng = DeviceAggregator(spec)
+    eng.corrupt_next_round()  # the first wave's first box fails its MAC
+    ck = tmp_path / "ck.safetensors"
+    st = StreamingAggregator(eng, wave=4, checkpoint=str(ck), checkpoint_every=1)
+    with pytest.raises(AggregationError, match="MAC"):
+        st.run(12, _waves(433, 5000))
+    assert not ck.exists()
