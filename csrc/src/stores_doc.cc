@@ -16,6 +16,7 @@
 //   participations {id, participation, snapshots: [SnapshotId]}
 //   snapshots      {id, snapshot, mask}
 //   clerking_jobs  {id, clerking_job, done, result}
+#include <algorithm>
 #include <map>
 #include <mutex>
 
@@ -41,11 +42,49 @@ const Value* path_get(const Value& doc, const std::string& path) {
   return cur;
 }
 
-// Mongo equality semantics: a field equals v, or (for arrays) contains v.
+// The string values a dotted path reaches in a document, Mongo style: arrays on
+// the way are traversed element by element ("keys.id" reaches the id of every
+// element of `keys`; "snapshots" reaches every snapshot id of the array).
+void collect_strings(const Value& v, const std::vector<std::string>& parts, size_t i,
+                     std::vector<std::string>& out) {
+  if (v.is_array()) {
+    for (auto& e : v.as_array()) collect_strings(e, parts, i, out);
+    return;
+  }
+  if (i == parts.size()) {
+    if (v.is_string()) out.push_back(v.as_string());
+    return;
+  }
+  if (!v.is_object()) return;
+  if (const Value* next = v.find(parts[i])) collect_strings(*next, parts, i + 1, out);
+}
+
+std::vector<std::string> split_path(const std::string& path) {
+  std::vector<std::string> parts;
+  size_t i = 0;
+  while (i <= path.size()) {
+    size_t j = path.find('.', i);
+    if (j == std::string::npos) j = path.size();
+    parts.push_back(path.substr(i, j - i));
+    i = j + 1;
+  }
+  return parts;
+}
+
+// Mongo equality semantics: a field equals v, or (for arrays) contains v; a
+// dotted path traverses arrays of sub-documents.
 bool matches(const Value& doc, const std::vector<std::pair<std::string, Value>>& filter) {
   for (auto& f : filter) {
     const Value* v = path_get(doc, f.first);
     if (!v) {
+      if (f.second.is_string()) {  // the path may run through an array of sub-documents
+        std::vector<std::string> got;
+        collect_strings(doc, split_path(f.first), 0, got);
+        bool found = false;
+        for (auto& g : got) found |= (g == f.second.as_string());
+        if (found) continue;
+        return false;
+      }
       if (!f.second.is_null()) return false;
       continue;
     }
@@ -61,33 +100,55 @@ bool matches(const Value& doc, const std::vector<std::pair<std::string, Value>>&
   return true;
 }
 
+// A collection with the unique `id` index of the reference DAO
+// (server-store-mongodb/src/lib.rs: `ensure_index` on `id`) and secondary
+// indexes on the string fields its queries filter on: find / count touch the
+// documents an index names, not the whole collection.
 class DocCollection {
  public:
-  DocCollection(std::string name, const std::string& dir) : name_(std::move(name)) {
+  DocCollection(std::string name, const std::string& dir, std::vector<std::string> indexed = {})
+      : name_(std::move(name)) {
+    for (auto& f : indexed) index_[f];
     if (!dir.empty()) {
       files_ = make_file_collection(dir + "/" + name_);
-      for (auto& kv : files_->all()) docs_[kv.first] = Value::parse(kv.second);
+      for (auto& kv : files_->all()) {
+        auto it = docs_.emplace(kv.first, Value::parse(kv.second)).first;
+        index_add(it->first, it->second);
+      }
     }
   }
   using Filter = std::vector<std::pair<std::string, Value>>;
 
   std::optional<Value> find_one(const Filter& f) {
     std::lock_guard<std::mutex> g(mu_);
-    for (auto& kv : docs_)
-      if (matches(kv.second, f)) return kv.second;
-    return std::nullopt;
+    std::optional<Value> out;
+    scan(f, [&](const std::string&, const Value& d) {
+      out = d;
+      return false;
+    });
+    return out;
   }
   std::vector<Value> find(const Filter& f) {
     std::lock_guard<std::mutex> g(mu_);
     std::vector<Value> out;
-    for (auto& kv : docs_)
-      if (matches(kv.second, f)) out.push_back(kv.second);
+    scan(f, [&](const std::string&, const Value& d) {
+      out.push_back(d);
+      return true;
+    });
     return out;
   }
   size_t count(const Filter& f) {
     std::lock_guard<std::mutex> g(mu_);
+    // a single indexed term: the index holds the answer
+    if (f.size() == 1 && f[0].second.is_string()) {
+      auto ix = index_.find(f[0].first);
+      if (ix != index_.end()) return ix->second.count(f[0].second.as_string());
+    }
     size_t n = 0;
-    for (auto& kv : docs_) n += matches(kv.second, f) ? 1 : 0;
+    scan(f, [&](const std::string&, const Value&) {
+      ++n;
+      return true;
+    });
     return n;
   }
   // {$set: fields} by id, optionally upserting (Dao::modisert_by_id / modify_by_id)
@@ -100,7 +161,9 @@ class DocCollection {
       d.set("id", Value(id));
       it = docs_.emplace(id, d).first;
     }
+    index_remove(id, it->second);
     for (auto& kv : fields) it->second.set(kv.first, kv.second);
+    index_add(id, it->second);
     persist(id, it->second);
     return true;
   }
@@ -110,35 +173,102 @@ class DocCollection {
     std::lock_guard<std::mutex> g(mu_);
     auto it = docs_.find(id);
     if (it == docs_.end()) return false;
+    index_remove(id, it->second);
     fn(it->second);
+    index_add(id, it->second);
     persist(id, it->second);
     return true;
   }
   template <class F>
   size_t update_many(const Filter& f, F fn) {
     std::lock_guard<std::mutex> g(mu_);
-    size_t n = 0;
-    for (auto& kv : docs_) {
-      if (!matches(kv.second, f)) continue;
-      fn(kv.second);
-      persist(kv.first, kv.second);
-      ++n;
+    std::vector<std::string> ids;
+    scan(f, [&](const std::string& id, const Value&) {
+      ids.push_back(id);
+      return true;
+    });
+    for (auto& id : ids) {
+      Value& d = docs_.at(id);
+      index_remove(id, d);
+      fn(d);
+      index_add(id, d);
+      persist(id, d);
     }
-    return n;
+    return ids.size();
   }
   bool delete_one(const std::string& id) {
     std::lock_guard<std::mutex> g(mu_);
     if (files_) files_->remove(id);
-    return docs_.erase(id) > 0;
+    auto it = docs_.find(id);
+    if (it == docs_.end()) return false;
+    index_remove(id, it->second);
+    docs_.erase(it);
+    return true;
   }
 
  private:
+  // Visit the documents matching `f` in id order until `visit` returns false.
+  // Candidates come from the `id` term or the most selective indexed term.
+  template <class V>
+  void scan(const Filter& f, V visit) {
+    for (auto& t : f)
+      if (t.first == "id" && t.second.is_string()) {
+        auto it = docs_.find(t.second.as_string());
+        if (it != docs_.end() && matches(it->second, f)) visit(it->first, it->second);
+        return;
+      }
+    const std::multimap<std::string, std::string>* best = nullptr;
+    const std::string* key = nullptr;
+    size_t best_n = 0;
+    for (auto& t : f) {
+      if (!t.second.is_string()) continue;
+      auto ix = index_.find(t.first);
+      if (ix == index_.end()) continue;
+      size_t n = ix->second.count(t.second.as_string());
+      if (!best || n < best_n) best = &ix->second, key = &t.second.as_string(), best_n = n;
+    }
+    if (best) {
+      std::vector<std::string> ids;
+      auto range = best->equal_range(*key);
+      for (auto it = range.first; it != range.second; ++it) ids.push_back(it->second);
+      std::sort(ids.begin(), ids.end());
+      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+      for (auto& id : ids) {
+        auto it = docs_.find(id);
+        if (it != docs_.end() && matches(it->second, f) && !visit(it->first, it->second)) return;
+      }
+      return;
+    }
+    for (auto& kv : docs_)
+      if (matches(kv.second, f) && !visit(kv.first, kv.second)) return;
+  }
+  void index_add(const std::string& id, const Value& d) {
+    for (auto& ix : index_) {
+      std::vector<std::string> vals;
+      collect_strings(d, split_path(ix.first), 0, vals);
+      for (auto& v : vals) ix.second.emplace(v, id);
+    }
+  }
+  void index_remove(const std::string& id, const Value& d) {
+    for (auto& ix : index_) {
+      std::vector<std::string> vals;
+      collect_strings(d, split_path(ix.first), 0, vals);
+      for (auto& v : vals) {
+        auto range = ix.second.equal_range(v);
+        for (auto it = range.first; it != range.second;) {
+          if (it->second == id) it = ix.second.erase(it);
+          else ++it;
+        }
+      }
+    }
+  }
   void persist(const std::string& id, const Value& d) {
     if (files_) files_->put(id, d.dump());
   }
   std::string name_;
   std::mutex mu_;
   std::map<std::string, Value> docs_;
+  std::map<std::string, std::multimap<std::string, std::string>> index_;  // field -> value -> ids
   std::shared_ptr<Collection> files_;
 };
 
@@ -157,7 +287,7 @@ std::optional<T> field_as(const std::optional<Value>& doc, const char* name) {
 // ---------------------------------------------------------------------------
 class DocAgentsStore : public AgentsStore {
  public:
-  explicit DocAgentsStore(const std::string& dir) : c_("agents", dir) {}
+  explicit DocAgentsStore(const std::string& dir) : c_("agents", dir, {"keys.id"}) {}
   void ping() override {}
   void create_agent(const Agent& a) override {
     auto prev = c_.find_one({{"id", Value(a.id.str())}});
@@ -192,18 +322,8 @@ class DocAgentsStore : public AgentsStore {
     if (!ok) throw SdaError("Agent not found for encryption key");
   }
   std::optional<SignedEncryptionKey> get_encryption_key(const EncryptionKeyId& id) override {
-    auto doc = c_.find_one({{"keys.id", Value(id.str())}});
-    if (!doc) {
-      // keys.id addresses elements of the keys array: scan
-      for (auto& d : c_.find({})) {
-        const Value* keys = d.find("keys");
-        if (!keys || !keys->is_array()) continue;
-        for (auto& e : keys->as_array())
-          if (e.find("id") && e.at("id") == Value(id.str()))
-            return wire::from_json<SignedEncryptionKey>(e.at("body"));
-      }
-      return std::nullopt;
-    }
+    auto doc = c_.find_one({{"keys.id", Value(id.str())}});  // indexed: the ids inside `keys`
+    if (!doc) return std::nullopt;
     for (auto& e : doc->at("keys").as_array())
       if (e.at("id") == Value(id.str())) return wire::from_json<SignedEncryptionKey>(e.at("body"));
     return std::nullopt;
@@ -243,7 +363,9 @@ class DocAuthTokensStore : public AuthTokensStore {
 class DocAggregationsStore : public AggregationsStore {
  public:
   explicit DocAggregationsStore(const std::string& dir)
-      : aggs_("aggregations", dir), parts_("participations", dir), snaps_("snapshots", dir) {}
+      : aggs_("aggregations", dir, {"aggregation.recipient"}),
+        parts_("participations", dir, {"participation.aggregation", "snapshots"}),
+        snaps_("snapshots", dir, {"snapshot.aggregation"}) {}
 
   std::vector<AggregationId> list_aggregations(const std::optional<std::string>& filter,
                                                const std::optional<AgentId>& recipient) override {
@@ -337,6 +459,11 @@ class DocAggregationsStore : public AggregationsStore {
     for (auto& e : mask) arr.push(wire::to_json(e));
     snaps_.set_by_id(s.str(), fields({{"mask", arr}}), false);
   }
+  std::optional<std::string> get_snapshot_mask_json(const SnapshotId& s) override {
+    auto doc = snaps_.find_one({{"id", Value(s.str())}});
+    if (!doc || !doc->find("mask") || doc->at("mask").is_null()) return std::nullopt;
+    return doc->at("mask").dump();
+  }
   std::optional<std::vector<Encryption>> get_snapshot_mask(const SnapshotId& s) override {
     auto doc = snaps_.find_one({{"id", Value(s.str())}});
     if (!doc || !doc->find("mask") || doc->at("mask").is_null()) return std::nullopt;
@@ -351,7 +478,8 @@ class DocAggregationsStore : public AggregationsStore {
 
 class DocClerkingJobsStore : public ClerkingJobsStore {
  public:
-  explicit DocClerkingJobsStore(const std::string& dir) : c_("clerking_jobs", dir) {}
+  explicit DocClerkingJobsStore(const std::string& dir)
+      : c_("clerking_jobs", dir, {"clerking_job.clerk", "clerking_job.snapshot"}) {}
   void enqueue_clerking_job(const ClerkingJob& j) override {
     c_.set_by_id(j.id.str(), fields({{"clerking_job", wire::to_json(j)}, {"done", Value(false)}}), true);
   }
@@ -365,6 +493,31 @@ class DocClerkingJobsStore : public ClerkingJobsStore {
                                               {"id", Value(job.str())},
                                               {"done", Value(false)}}),
                                  "clerking_job");
+  }
+  // bulk forms: the stored sub-documents are dumped as they are, the boxes are
+  // never decoded on the server
+  std::optional<std::string> poll_clerking_job_json(const AgentId& clerk) override {
+    auto doc = c_.find_one({{"done", Value(false)}, {"clerking_job.clerk", Value(clerk.str())}});
+    if (!doc || !doc->find("clerking_job")) return std::nullopt;
+    return doc->at("clerking_job").dump();
+  }
+  std::optional<ClerkingJob> get_clerking_job_head(const AgentId& clerk, const ClerkingJobId& job) override {
+    auto doc = c_.find_one({{"clerking_job.clerk", Value(clerk.str())},
+                            {"id", Value(job.str())},
+                            {"done", Value(false)}});
+    if (!doc) return std::nullopt;
+    const Value& j = doc->at("clerking_job");
+    ClerkingJob head;
+    head.id = ClerkingJobId::parse(j.at("id").as_string());
+    head.clerk = AgentId::parse(j.at("clerk").as_string());
+    head.aggregation = AggregationId::parse(j.at("aggregation").as_string());
+    head.snapshot = SnapshotId::parse(j.at("snapshot").as_string());
+    return head;
+  }
+  std::optional<std::string> get_result_json(const SnapshotId& s, const ClerkingJobId& job) override {
+    auto doc = c_.find_one({{"clerking_job.snapshot", Value(s.str())}, {"id", Value(job.str())}});
+    if (!doc || !doc->find("result") || doc->at("result").is_null()) return std::nullopt;
+    return doc->at("result").dump();
   }
   void create_clerking_result(const ClerkingResult& r) override {
     if (!c_.update_by_id(r.job.str(), [&](Value& doc) {
