@@ -260,6 +260,9 @@ class Backend final : public DeviceBackend {
                   const uint32_t* pks, uint32_t* err);
   Keys seal_setup(Lease& mem, const Arena& a, const uint32_t* key_idx, const uint32_t* pks,
                   uint64_t owner_base, const RngKeyArg& rng, uint32_t* err);
+  void tables(Lease& mem, const Arena& a, Keys& k);
+  void verify_decrypt(Lease& mem, const Arena& a, const Keys& k, uint32_t* term, uint32_t* pre,
+                      uint32_t* err);
   void open_sum(Lease& mem, const Arena& a, const Keys& k, int rows, uint32_t* out, uint32_t* err);
   void open_data(Lease& mem, const Arena& a, const Keys& k, uint32_t* out, uint32_t* err);
   void seal_data(Lease& mem, const Arena& a, const Keys& k, const void* values, int value_bytes,
@@ -391,15 +394,47 @@ void Backend::check(uint32_t* err_dev, const char* what) {
 }
 
 // ------------------------------------------------------------ kernel sequences ----
+// Poly1305 tables of a key set: the one-pass form (r^1 .. r^64) for boxes of at most
+// kShortMaxChunks chunks, the chunked MAC's 26 KB per box otherwise.
+static bool short_boxes(const Arena& a) { return a.K <= kShortMaxChunks; }
+
+void Backend::tables(Lease& mem, const Arena& a, Keys& k) {
+  if (short_boxes(a)) {
+    k.pows = mem.take<uint32_t>((size_t)a.M * kPowShortWords);
+    launch_poly_powers_short(a.M, k.keys, k.pows, s_);
+    launched("poly_powers_short");
+  } else {
+    k.pows = mem.take<uint32_t>((size_t)a.M * kPowWords);
+    launch_poly_powers(a.M, k.keys, k.pows, 1, s_);
+    launched("poly_powers");
+  }
+}
+
+// Tag check, then in-place decryption with terminator counts (per chunk / sub-chunk).
+void Backend::verify_decrypt(Lease& mem, const Arena& a, const Keys& k, uint32_t* term,
+                             uint32_t* pre, uint32_t* err) {
+  const int M = a.M, K = a.K;
+  if (short_boxes(a)) {
+    launch_mac_short(M, k.keys, k.pows, a.ct, a.stride, a.pt_len, 1, nullptr, err, s_);
+    launched("mac_short");
+    launch_decrypt_count(M, K, k.keys, a.ct, a.stride, a.pt_len, term, pre, s_);
+    launched("decrypt_count");
+    return;
+  }
+  uint32_t* partials = mem.take<uint32_t>((size_t)M * K * 8);
+  launch_mac_chunks(M, K, k.keys, k.pows, a.ct, a.stride, a.pt_len, partials, 1, term, pre, s_);
+  launched("mac_chunks");
+  launch_mac_final(M, K, k.keys, k.pows, a.ct, a.stride, a.pt_len, partials, 1, nullptr, err, s_);
+  launched("mac_final");
+}
+
 Keys Backend::open_setup(Lease& mem, const Arena& a, const uint32_t* key_idx, const uint32_t* sks,
                          const uint32_t* pks, uint32_t* err) {
   Keys k;
   k.keys = mem.take<MsgKey>(a.M);
-  k.pows = mem.take<uint32_t>((size_t)a.M * kPowWords);
   launch_open_setup(a.M, key_idx, sks, pks, a.ct, a.stride, k.keys, err, nullptr, 0, s_);
   launched("open_setup");
-  launch_poly_powers(a.M, k.keys, k.pows, a.K > 2 ? 1 : 0, s_);
-  launched("poly_powers");
+  tables(mem, a, k);
   return k;
 }
 
@@ -407,11 +442,9 @@ Keys Backend::seal_setup(Lease& mem, const Arena& a, const uint32_t* key_idx, co
                          uint64_t owner_base, const RngKeyArg& rng, uint32_t* err) {
   Keys k;
   k.keys = mem.take<MsgKey>(a.M);
-  k.pows = mem.take<uint32_t>((size_t)a.M * kPowWords);
   launch_seal_setup(a.M, rng, owner_base, key_idx, pks, a.ct, a.stride, k.keys, err, nullptr, 0, s_);
   launched("seal_setup");
-  launch_poly_powers(a.M, k.keys, k.pows, a.K > 2 ? 1 : 0, s_);
-  launched("poly_powers");
+  tables(mem, a, k);
   return k;
 }
 
@@ -420,12 +453,8 @@ void Backend::open_sum(Lease& mem, const Arena& a, const Keys& k, int rows, uint
   const int M = a.M, K = a.K, P = M / rows;
   const int S = K * kSubPerChunk;
   const int L = (int)a.L;
-  uint32_t* partials = mem.take<uint32_t>((size_t)M * K * 8);
   uint32_t* pre = mem.take<uint32_t>((size_t)M * S);
-  launch_mac_chunks(M, K, k.keys, k.pows, a.ct, a.stride, a.pt_len, partials, 1, nullptr, pre, s_);
-  launched("mac_chunks");
-  launch_mac_final(M, K, k.keys, k.pows, a.ct, a.stride, a.pt_len, partials, 1, nullptr, err, s_);
-  launched("mac_final");
+  verify_decrypt(mem, a, k, nullptr, pre, err);
   uint32_t* totals = mem.take<uint32_t>(M);
   launch_segscan(M, S, pre, totals, (uint32_t)L, err, s_);  // exactly L values per box
   launched("segscan");
@@ -444,12 +473,8 @@ void Backend::open_sum(Lease& mem, const Arena& a, const Keys& k, int rows, uint
 
 void Backend::open_data(Lease& mem, const Arena& a, const Keys& k, uint32_t* out, uint32_t* err) {
   const int M = a.M, K = a.K, L = (int)a.L;
-  uint32_t* partials = mem.take<uint32_t>((size_t)M * K * 8);
   uint32_t* term = mem.take<uint32_t>((size_t)M * K);
-  launch_mac_chunks(M, K, k.keys, k.pows, a.ct, a.stride, a.pt_len, partials, 1, term, nullptr, s_);
-  launched("mac_chunks");
-  launch_mac_final(M, K, k.keys, k.pows, a.ct, a.stride, a.pt_len, partials, 1, nullptr, err, s_);
-  launched("mac_final");
+  verify_decrypt(mem, a, k, term, nullptr, err);
   uint32_t* totals = mem.take<uint32_t>(M);
   launch_segscan(M, K, term, totals, (uint32_t)L, err, s_);
   launched("segscan");
@@ -471,6 +496,11 @@ void Backend::seal_data(Lease& mem, const Arena& a, const Keys& k, const void* v
   launch_encode_encrypt(M, L, value_bytes, values, cnt, k.keys, a.ct, a.stride, nullptr, nullptr,
                         nullptr, 0, s_);
   launched("encode_encrypt");
+  if (short_boxes(a)) {
+    launch_mac_short(M, k.keys, k.pows, a.ct, a.stride, a.pt_len, 0, nullptr, err, s_);
+    launched("mac_short");
+    return;
+  }
   uint32_t* partials = mem.take<uint32_t>((size_t)M * K * 8);
   launch_mac_chunks(M, K, k.keys, k.pows, a.ct, a.stride, a.pt_len, partials, 0, nullptr, nullptr, s_);
   launched("mac_chunks");
@@ -579,7 +609,7 @@ std::vector<int64_t> Backend::reveal(const Aggregation& agg, const EncryptionKey
       launch_limbs_t(nI, (int)B, Kp, limbs, ys, X, s_);
       launched("limbs_t");
       launch_modgemm_i8((int)k, (int)B, Kp, 1, limbs, m, dA, X, (int64_t)B * Kp, 4, masked, 0, 1,
-                        (int64_t)k, (int64_t)D, s_);
+                        (int64_t)k, (int64_t)D, nullptr, s_);
       launched("modgemm_i8");
       sync();
     }
@@ -676,8 +706,11 @@ DeviceParticipations Backend::participate_many(const Aggregation& agg,
   // participants per wave: arenas, shares and tables within about half of the free memory
   size_t free_b = 0, total_b = 0;
   HIP_OK(hipMemGetInfo(&free_b, &total_b));
-  size_t per_p = (size_t)n * (stride + B * value_bytes + (size_t)kPowWords * 4 + 256) + D * 4 * 2 +
-                 (mask_mode == kMaskFull ? slot_stride(D, m) + D * 4 + (size_t)kPowWords * 4 : 0) +
+  auto table_bytes = [&](size_t L) {
+    return (size_t)4 * (chunks_for(L * (size_t)varint_max_len(m)) <= kShortMaxChunks ? kPowShortWords : kPowWords);
+  };
+  size_t per_p = (size_t)n * (stride + B * value_bytes + table_bytes(B) + 256) + D * 4 * 2 +
+                 (mask_mode == kMaskFull ? slot_stride(D, m) + D * 4 + table_bytes(D) : 0) +
                  (big ? (size_t)(m < (1u << 21) ? 3 : 4) * B * ((k + t_priv + 63) / 64 * 64) : 0);
   size_t wave = std::max<size_t>(1, std::min<size_t>(inputs.size(), (free_b / 2) / std::max<size_t>(1, per_p)));
 
@@ -708,7 +741,7 @@ DeviceParticipations Backend::participate_many(const Aggregation& agg,
     void* mask_out = mask_mode == kMaskFull ? mem.take<uint8_t>((size_t)P * D * mask_bytes) : nullptr;
     uint32_t* mask_cnt = mask_mode == kMaskFull ? mem.take<uint32_t>((size_t)P * tiles(D)) : nullptr;
     uint32_t* seeds = mask_mode == kMaskChaCha ? mem.take<uint32_t>((size_t)P * seed_words) : nullptr;
-    bool have_cnt = true, have_mask_cnt = mask_mode == kMaskFull;
+    bool have_mask_cnt = mask_mode == kMaskFull;
     int share_mode = mask_mode;
     if (mask_mode == kMaskChaCha) {
       // chacha.rs:29-45 as a pre-pass: fresh seeds, masked = secret + the seed's stream;
@@ -755,10 +788,12 @@ DeviceParticipations Backend::participate_many(const Aggregation& agg,
       int8_t* X = mem.take<int8_t>((size_t)limbs * P * B * Kp);
       launch_pss_x_limbs(P, (int)D, (int)B, (int)k, t_priv, Kp, limbs, m, masked, rng, 0, X, s_);
       launched("pss_x_limbs");
+      // the boxes' varint bytes come out of the GEMM epilogue (cnt zeroed first; this
+      // backend never runs inside a captured graph)
+      HIP_OK(hipMemsetAsync(cnt, 0, (size_t)n * P * tiles(B) * sizeof(uint32_t), s_));
       launch_modgemm_i8(n, (int)B, Kp, P, limbs, m, dA, X, (int64_t)P * B * Kp, value_bytes, shares,
-                        (int64_t)B, (int64_t)P * B, 1, (int64_t)n * P * B, s_);
+                        (int64_t)B, (int64_t)P * B, 1, (int64_t)n * P * B, cnt, s_);
       launched("modgemm_i8");
-      have_cnt = false;
       sync();
     }
     // ---- seal: slot c * P + p = participant p's box for clerk c (participate.rs:82-101)
@@ -770,7 +805,7 @@ DeviceParticipations Backend::participate_many(const Aggregation& agg,
     for (auto& ck : clerk_keys) kp.push_back(ck.sodium.data());
     uint32_t* pks = key_words(mem, kp);
     Keys ks = seal_setup(mem, arena, dkidx, pks, 0, rng, err);
-    seal_data(mem, arena, ks, shares, value_bytes, have_cnt ? cnt : nullptr, err);
+    seal_data(mem, arena, ks, shares, value_bytes, cnt, err);
     Arena marena;
     if (mask_mode != kMaskNone) {
       const bool full = mask_mode == kMaskFull;

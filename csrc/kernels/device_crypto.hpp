@@ -543,6 +543,25 @@ SDA_DEV Fe10 fe10_sub(const Fe10& a, const Fe10& b) {
   }
   return fe10_carry(r);
 }
+// The same without the carry pass, for results that go straight into a product:
+// with carried inputs (even limbs <= 2^26, odd <= 2^25, plus a few units) a sum has
+// limbs <= 2^27 / 2^26 and a difference <= 3 * 2^26 / 3 * 2^25; fe10_mul / fe10_sq of
+// two such operands keep 19 f < 2^32 and every column sum below 1120 * 2^52 < 2^63.
+SDA_DEV Fe10 fe10_add_nc(const Fe10& a, const Fe10& b) {
+  Fe10 r;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) r.v[i] = a.v[i] + b.v[i];
+  return r;
+}
+SDA_DEV Fe10 fe10_sub_nc(const Fe10& a, const Fe10& b) {
+  Fe10 r;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t two_p = (i == 0) ? 0x7ffffdau : ((i & 1) ? 0x3fffffeu : 0x7fffffeu);
+    r.v[i] = a.v[i] + two_p - b.v[i];
+  }
+  return r;
+}
 SDA_DEV Fe10 fe10_mul(const Fe10& f, const Fe10& g) {
   uint32_t g19[10], f2[10];
 #pragma unroll
@@ -688,15 +707,16 @@ SDA_DEV void x25519(uint32_t (&out)[8], const uint32_t (&scalar)[8], const uint3
     fe10_cswap(x2, x3, swap);
     fe10_cswap(z2, z3, swap);
     swap = kt;
-    const Fe10 A = fe10_add(x2, z2), B = fe10_sub(x2, z2);
-    const Fe10 C = fe10_add(x3, z3), D = fe10_sub(x3, z3);
+    // every sum / difference feeds a product directly: no carry passes (fe10_add_nc)
+    const Fe10 A = fe10_add_nc(x2, z2), B = fe10_sub_nc(x2, z2);
+    const Fe10 C = fe10_add_nc(x3, z3), D = fe10_sub_nc(x3, z3);
     const Fe10 AA = fe10_sq(A), BB = fe10_sq(B);
     const Fe10 DA = fe10_mul(D, A), CB = fe10_mul(C, B);
-    const Fe10 E = fe10_sub(AA, BB);
-    x3 = fe10_sq(fe10_add(DA, CB));
-    z3 = fe10_mul(x1, fe10_sq(fe10_sub(DA, CB)));
+    const Fe10 E = fe10_sub_nc(AA, BB);
+    x3 = fe10_sq(fe10_add_nc(DA, CB));
+    z3 = fe10_mul(x1, fe10_sq(fe10_sub_nc(DA, CB)));
     x2 = fe10_mul(AA, BB);
-    z2 = fe10_mul(E, fe10_add(AA, fe10_mul121665(E)));
+    z2 = fe10_mul(E, fe10_add_nc(AA, fe10_mul121665(E)));
   }
   fe10_cswap(x2, x3, swap);
   fe10_cswap(z2, z3, swap);

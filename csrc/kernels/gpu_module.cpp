@@ -186,6 +186,24 @@ PYBIND11_MODULE(_sda_gpu, m) {
                       P<uint32_t>(term_cnt), P<uint32_t>(sub_cnt), S(stream));
     check_launch("mac_chunks");
   });
+  m.def("poly_powers_short", [](int M, uintptr_t keys, uintptr_t pows, uintptr_t stream) {
+    launch_poly_powers_short(M, P<const MsgKey>(keys), P<uint32_t>(pows), S(stream));
+    check_launch("poly_powers_short");
+  });
+  m.def("mac_short", [](int M, uintptr_t keys, uintptr_t pows, uintptr_t ct, uint64_t stride,
+                        uintptr_t pt_len, int verify, uintptr_t ok, uintptr_t err, uintptr_t stream) {
+    launch_mac_short(M, P<const MsgKey>(keys), P<const uint32_t>(pows), P<uint8_t>(ct), stride,
+                     P<const uint32_t>(pt_len), verify, P<uint32_t>(ok), P<uint32_t>(err), S(stream));
+    check_launch("mac_short");
+  });
+  m.def("decrypt_count", [](int M, int K, uintptr_t keys, uintptr_t ct, uint64_t stride,
+                            uintptr_t pt_len, uintptr_t term_cnt, uintptr_t sub_cnt,
+                            uintptr_t stream) {
+    launch_decrypt_count(M, K, P<const MsgKey>(keys), P<uint8_t>(ct), stride,
+                         P<const uint32_t>(pt_len), P<uint32_t>(term_cnt), P<uint32_t>(sub_cnt),
+                         S(stream));
+    check_launch("decrypt_count");
+  });
   m.def("mac_final", [](int M, int K, uintptr_t keys, uintptr_t pows, uintptr_t ct, uint64_t stride,
                         uintptr_t pt_len, uintptr_t partials, int verify, uintptr_t ok,
                         uintptr_t err, uintptr_t stream) {
@@ -205,6 +223,8 @@ PYBIND11_MODULE(_sda_gpu, m) {
   m.attr("SUB_BYTES") = kSubBytes;
   m.attr("SUM_TILE") = kSumTile;
   m.attr("POW_WORDS") = kPowWords;
+  m.attr("POW_SHORT_WORDS") = kPowShortWords;
+  m.attr("SHORT_MAX_CHUNKS") = kShortMaxChunks;
   m.def("locate_tiles", [](int M, int Sn, int L, uintptr_t pre, uintptr_t totals,
                            uintptr_t tile_sub, uintptr_t stream) {
     launch_locate_tiles(M, Sn, L, P<const uint32_t>(pre), P<const uint32_t>(totals),
@@ -230,6 +250,8 @@ PYBIND11_MODULE(_sda_gpu, m) {
     check_launch("decode_sum");
   });
   m.def("set_decode_lean", &set_decode_lean);
+  m.def("set_decode_swz", &set_decode_swz);
+  m.def("set_gemm_fold24", &set_gemm_fold24);
   m.def("colsum", [](int G, int R, int L, uint32_t mod, int value_bytes, uintptr_t vals,
                      uintptr_t out, uintptr_t stream) {
     launch_colsum(G, R, L, mod, value_bytes, P<const void>(vals), P<uint32_t>(out), S(stream));
@@ -244,14 +266,14 @@ PYBIND11_MODULE(_sda_gpu, m) {
   m.def("modgemm_i8", [](int M, int N, int Kp, int batches, int limbs, uint32_t prime,
                          uintptr_t A, uintptr_t B, int64_t b_plane, int value_bytes, uintptr_t C,
                          int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit,
-                         uintptr_t stream) {
+                         uintptr_t cnt, uintptr_t stream) {
     if (Kp % 64 != 0) throw std::invalid_argument("modgemm_i8: Kp must be a multiple of 64");
     if (limbs != 3 && limbs != 4) throw std::invalid_argument("modgemm_i8: limbs must be 3 or 4");
     if (prime >= (1u << (7 * limbs))) throw std::invalid_argument("modgemm_i8: modulus too large");
     if ((int64_t)Kp * 127 * 127 * limbs >= (int64_t)1 << 31)
       throw std::invalid_argument("modgemm_i8: K too large for int32 limb accumulators");
     launch_modgemm_i8(M, N, Kp, batches, limbs, prime, P<const int8_t>(A), P<const int8_t>(B), b_plane,
-                      value_bytes, P<void>(C), ldc_z, ldc_m, ldc_n, limit, S(stream));
+                      value_bytes, P<void>(C), ldc_z, ldc_m, ldc_n, limit, P<uint32_t>(cnt), S(stream));
     check_launch("modgemm_i8");
   });
   m.def("pss_x_limbs", [](int Pn, int D, int B, int k, int t, int Kp, int limbs, uint32_t prime,

@@ -376,7 +376,7 @@ int main() {
     CHECK(std::memcmp(b2, db2, 24) == 0, "blake2b");
   }
   // 1b. device X25519 (radix 2^25.5 ladder) vs host
-  for (int it = 0; it < 32; ++it) {
+  for (int it = 0; it < 256; ++it) {
     uint8_t sc[32], pt[32], ho[32];
     hc::os_random(sc, 32);
     hc::os_random(pt, 32);

@@ -54,6 +54,11 @@ constexpr int kPowRowOff = kPowTabOff + kPolyDigits * kSegBytes / 4;
 constexpr int kPowQOff = kPowRowOff + 16 * 5;
 constexpr int kPowWords = (kPowQOff + 65 * 5 + 7) / 8 * 8;
 
+// Messages of at most kShortMaxChunks chunks (64 KiB) take the one-pass MAC
+// (k_mac_short) with its own, small table: r^(t+1), t < 64, 5 limbs each.
+constexpr int kShortMaxChunks = 4;
+constexpr int kPowShortWords = 64 * 5;
+
 // Error bits (device error word)
 enum ErrBits : uint32_t {
   kErrBadKey = 1u,          // X25519 produced the all-zero point
@@ -172,6 +177,17 @@ void launch_poly_powers(int M, const MsgKey* keys, uint32_t* pows, int full, hip
 void launch_mac_chunks(int M, int K, const MsgKey* keys, const uint32_t* pows, uint8_t* ct,
                        uint64_t stride, const uint32_t* pt_len, uint32_t* partials, int decrypt,
                        uint32_t* term_cnt, uint32_t* sub_cnt, hipStream_t s);
+// One-pass Poly1305 of short messages (any length works; meant for at most
+// kShortMaxChunks chunks): pows [M][kPowShortWords] from launch_poly_powers_short;
+// verify == 0 writes the tag into the header, else compares (ok[j] may be null, a
+// mismatch raises kErrMac). Reads the ciphertext: run it before the decryption.
+void launch_poly_powers_short(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s);
+void launch_mac_short(int M, const MsgKey* keys, const uint32_t* pows, uint8_t* ct, uint64_t stride,
+                      const uint32_t* pt_len, int verify, uint32_t* ok, uint32_t* err, hipStream_t s);
+// In-place decryption + terminator counts alone (launch_mac_chunks without its MAC).
+void launch_decrypt_count(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,
+                          const uint32_t* pt_len, uint32_t* term_cnt, uint32_t* sub_cnt,
+                          hipStream_t s);
 // Matrix-core Poly1305 segments (default on; 0 = per-lane Horner everywhere) --
 // benchmarking switch.
 void set_mac_mfma(int mode);
@@ -202,6 +218,8 @@ void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* p
                        hipStream_t s);  // acc != null: acc[r][l] += the sums instead of writing out
 // Lean clerk decode (default on; 0 = generic kernel only) -- benchmarking switch.
 void set_decode_lean(int mode);
+// lean decode-sum accumulator layout: -1 padded rows by modulus (default), 0 never, 1 always
+void set_decode_swz(int mode);
 // Column sums mod m: out[g][l] = sum_r vals[g][r][l] mod m.
 void launch_colsum(int G, int R, int L, uint32_t m, int value_bytes, const void* vals,
                    uint32_t* out, hipStream_t s);
@@ -217,9 +235,14 @@ void launch_sub_mod(int D, uint32_t m, const uint32_t* a, const uint32_t* b, uin
 // C = A . B mod p (p < 2^28) on i8 MFMA with `limbs` (3 or 4) 7-bit limbs. A limbs
 // [L][M][Kp], B limbs [L][batches][N][Kp] (b_plane = batches*N*Kp bytes between limb
 // planes), C[z*ldc_z + m*ldc_m + n*ldc_n] written where that index < limit.
+// cnt (may be null; zeroed by the caller): [M][batches][ceil(N / kTileValues)] varint
+// bytes of the written elements, i.e. launch_count's result for C as M x batches
+// messages of N values (the share GEMM: rows = clerks, batches = participants).
 void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p, const int8_t* A,
                        const int8_t* B, int64_t b_plane, int value_bytes, void* C, int64_t ldc_z,
-                       int64_t ldc_m, int64_t ldc_n, int64_t limit, hipStream_t s);
+                       int64_t ldc_m, int64_t ldc_n, int64_t limit, uint32_t* cnt, hipStream_t s);
+// epilogue reductions on the 24-bit multipliers where the modulus allows (default on)
+void set_gemm_fold24(int on);
 // X limbs [3][P][B][Kp] of packed-Shamir inputs: secrets (canonical) then t draws.
 void launch_pss_x_limbs(int P, int D, int B, int k, int t, int Kp, int limbs, uint32_t p,
                         const int32_t* secrets, RngKeyArg rng, uint64_t owner_base, int8_t* X,

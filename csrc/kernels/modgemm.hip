@@ -29,6 +29,13 @@
 // MFMAs: with p < 2^21 the 2L - 1 degree sums fold by a 32-bit Horner chain
 // (s <- (s * 2^7 + acc_d) mod p, every intermediate below 2^32) instead of
 // 64-bit multiply-adds.
+//
+// Share generation also needs every sealed box's varint length per 4096-value
+// tile before the encoder can place its bytes (kernels.hpp, launch_count). With
+// `cnt` the epilogue adds them up itself -- the lengths of a lane's outputs per
+// row, summed over the 16 lanes of a row group on the VALU (DPP), one atomic add
+// per (row, wave) -- instead of a second pass over the stored shares.
+#include "block_utils.hpp"
 #include "device_crypto.hpp"
 #include "kernels.hpp"
 #include "modarith.hpp"
@@ -45,11 +52,16 @@ SDA_DEV int swz(int row, int chunk) {  // position of a row's 16-byte chunk insi
   return chunk ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3);  // {0, 2, 3, 1}
 }
 
-template <typename VT, int kLimbs>
+// kFold: how the epilogue folds the degree sums. 0: Horner chain with mod32 (p <
+// 2^24: s < p and acc_d < 2^31 keep s * 2^7 + acc_d below 2^32); 1: the same chain on
+// the 24-bit multipliers (mod24w, 2^16 <= p < 2^24: both of the reference's large
+// fields); 2: 64-bit multiply-adds by 2^(7d) mod p and one 64-bit reduction (p >= 2^24).
+template <typename VT, int kLimbs, int kFold>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
-    k_modgemm_i8(int M, int N, int Kp, ModParams mp, const int8_t* __restrict__ A,
+    k_modgemm_i8(int M, int N, int Kp, ModParams mp, Mod24w m24, const int8_t* __restrict__ A,
                  const int8_t* __restrict__ B, int64_t b_batch, VT* __restrict__ C,
-                 int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit) {
+                 int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit,
+                 uint32_t* __restrict__ cnt, int cnt_tiles) {
   constexpr int kRows = kBM + kBN;                       // staged rows per limb
   constexpr int kStage = kLimbs * kRows * kBK;           // bytes per buffer
   constexpr int kDeg = 2 * kLimbs - 1;
@@ -142,12 +154,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // built from per-lane bases by additions (the general z/m/n strides would cost
   // three 64-bit multiplies per element otherwise).
   uint32_t w[kDeg];
+  if constexpr (kFold == 2) {
 #pragma unroll
-  for (int d = 0; d < kDeg; ++d) w[d] = (uint32_t)(((uint64_t)1 << (kLimbBits * d)) % mp.m);
+    for (int d = 0; d < kDeg; ++d) w[d] = (uint32_t)(((uint64_t)1 << (kLimbBits * d)) % mp.m);
+  }
+  auto red = [&](uint32_t x) -> uint32_t {
+    if constexpr (kFold == 1) return mod24w(x, m24);
+    else return mod32(x, mp);
+  };
   const int row0 = m_blk + wm * 32 + 4 * (lane >> 4);
   const int col0 = n_blk + wn * 64 + (lane & 15);
   const int64_t base = (int64_t)z * ldc_z + (int64_t)row0 * ldc_m + (int64_t)col0 * ldc_n;
   const int64_t step_j = 16 * ldc_n, step_i = 16 * ldc_m;
+  uint32_t bytes[2][2] = {{0, 0}, {0, 0}};  // varint bytes of rows (i, r): two 16-bit sums per word
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -159,11 +178,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int j = 0; j < 4; ++j, idx += step_j) {
         if (col0 + 16 * j >= N) continue;
         uint32_t out;
-        if constexpr (kLimbs == 3) {
-          // acc_d < 2^31, s < p < 2^21: s * 2^7 + acc_d < 2^32
-          uint32_t s = mod32((uint32_t)acc[i][j][kDeg - 1][r], mp);
+        if constexpr (kFold != 2) {
+          // acc_d < 2^31, s < p < 2^24: s * 2^7 + acc_d < 2^32
+          uint32_t s = red((uint32_t)acc[i][j][kDeg - 1][r]);
 #pragma unroll
-          for (int d = kDeg - 2; d >= 0; --d) s = mod32((s << kLimbBits) + (uint32_t)acc[i][j][d][r], mp);
+          for (int d = kDeg - 2; d >= 0; --d) s = red((s << kLimbBits) + (uint32_t)acc[i][j][d][r]);
           out = s;
         } else {
           uint64_t s = 0;
@@ -172,7 +191,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
             s += (uint64_t)mod32((uint32_t)acc[i][j][d][r], mp) * w[d];  // < 7 * 2^56
           out = mod64(s, mp);
         }
-        if (idx < limit) C[idx] = (VT)out;
+        if (idx < limit) {
+          C[idx] = (VT)out;
+          // zigzag code 2 * out: one byte below 2^6, two below 2^13, ...
+          uint32_t len = 1u + (out >= (1u << 6)) + (out >= (1u << 13)) + (out >= (1u << 20));
+          if constexpr (kLimbs > 3) len += out >= (1u << 27);
+          bytes[i][r >> 1] += len << (16 * (r & 1));
+        }
+      }
+    }
+  if (cnt == nullptr) return;  // uniform
+  // the block's 128 columns lie inside one count tile (kTileValues is a multiple of kBN)
+  static_assert(kTileValues % kBN == 0, "a block's columns must not straddle a count tile");
+  const int tile = n_blk / kTileValues;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // a row's 64 columns of this wave: 4 per lane, over the 16 lanes of the row group
+      const uint32_t sum = row16_incl_scan(bytes[i][h]);
+      if ((lane & 15) != 15) continue;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int row = row0 + 16 * i + 2 * h + q;
+        const uint32_t v = (sum >> (16 * q)) & 0xffffu;
+        if (row < M && v != 0)
+          atomicAdd(&cnt[((int64_t)row * gridDim.z + z) * cnt_tiles + tile], v);
       }
     }
 }
@@ -257,22 +301,37 @@ __global__ void __launch_bounds__(256)
 
 }  // namespace
 
+static int g_gemm_fold24 = 1;
+void set_gemm_fold24(int on) { g_gemm_fold24 = on; }
+
 void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p, const int8_t* A,
                        const int8_t* B, int64_t b_plane, int value_bytes, void* C, int64_t ldc_z,
-                       int64_t ldc_m, int64_t ldc_n, int64_t limit, hipStream_t s) {
+                       int64_t ldc_m, int64_t ldc_n, int64_t limit, uint32_t* cnt, hipStream_t s) {
   if (M <= 0 || N <= 0 || batches <= 0) return;
   ModParams mp = make_mod_params(p);
+  const Mod24w m24 = make_mod24w(p);
+  const int fold = p >= (1u << 24) ? 2 : (m24.mu != 0 && g_gemm_fold24 ? 1 : 0);
   dim3 grid((N + kBN - 1) / kBN, (M + kBM - 1) / kBM, batches);
-#define SDA_GEMM(VT, L)                                                                      \
-  hipLaunchKernelGGL((k_modgemm_i8<VT, L>), grid, dim3(256), 0, s, M, N, Kp, mp, A, B, b_plane, \
-                     (VT*)C, ldc_z, ldc_m, ldc_n, limit)
-  if (value_bytes == 1) {
-    if (limbs == 3) SDA_GEMM(uint8_t, 3); else SDA_GEMM(uint8_t, 4);
-  } else if (value_bytes == 2) {
-    if (limbs == 3) SDA_GEMM(uint16_t, 3); else SDA_GEMM(uint16_t, 4);
-  } else {
-    if (limbs == 3) SDA_GEMM(uint32_t, 3); else SDA_GEMM(uint32_t, 4);
-  }
+  const int cnt_tiles = (N + kTileValues - 1) / kTileValues;
+#define SDA_GEMM(VT, L, F)                                                                        \
+  hipLaunchKernelGGL((k_modgemm_i8<VT, L, F>), grid, dim3(256), 0, s, M, N, Kp, mp, m24, A, B, b_plane, \
+                     (VT*)C, ldc_z, ldc_m, ldc_n, limit, cnt, cnt_tiles)
+#define SDA_GEMM_VT(VT)                                                     \
+  do {                                                                      \
+    if (limbs == 3) {                                                       \
+      if (fold == 1) SDA_GEMM(VT, 3, 1); else SDA_GEMM(VT, 3, 0);           \
+    } else if (fold == 2) {                                                 \
+      SDA_GEMM(VT, 4, 2);                                                   \
+    } else if (fold == 1) {                                                 \
+      SDA_GEMM(VT, 4, 1);                                                   \
+    } else {                                                                \
+      SDA_GEMM(VT, 4, 0);                                                   \
+    }                                                                       \
+  } while (0)
+  if (value_bytes == 1) SDA_GEMM_VT(uint8_t);
+  else if (value_bytes == 2) SDA_GEMM_VT(uint16_t);
+  else SDA_GEMM_VT(uint32_t);
+#undef SDA_GEMM_VT
 #undef SDA_GEMM
 }
 

@@ -244,7 +244,16 @@ SDA_DEV uint32_t spread4(uint32_t bits4) {  // 4 bits -> 0xff per set bit, byte 
 // continuation bytes right before it), a lane leaves the run of up to three
 // continuation bytes at its end to the next lane, which adds them from the four
 // bytes before its own; five-byte varints raise `redo`.
-template <int kMaxBytes>
+//
+// kSwz: the accumulator with one pad word after every 32 (rank x at word
+// x + (x >> 5)). A lane's 64 bytes hold 64 / (code length) elements, so with codes
+// that are (nearly) all two, three or four bytes long the lanes' ranks are 32,
+// 21.33 or 16 words apart and the same ds_add of every lane falls into one, three
+// or two banks; in 33-word rows those strides step through all of them. Costs two
+// VALU instructions per add: used for the long codes and for moduli whose codes are
+// nearly all two bytes (m > 2048), not for the small moduli with their mix of one-
+// and two-byte codes (irregular strides already).
+template <int kMaxBytes, bool kSwz>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMaxBytes > 2 ? 3 : 4)))
     k_decode_sum_z(int L, int P, int Pg, const uint8_t* __restrict__ pt, uint64_t stride,
                    const uint32_t* __restrict__ pt_len, int S, const uint32_t* __restrict__ pre,
@@ -253,14 +262,19 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMa
   // three (kMaxBytes = 4 only): the field's codes have at most three bytes, a fourth
   // raises `redo` (the caller sized the participant groups for 21-bit codes)
   constexpr int kWaveBytes = 64 * 64;
-  __shared__ uint32_t acc[kSumAcc];
+  constexpr int kAccWords = kSwz ? kSumAcc + kSumAcc / 32 + 1 : kSumAcc;
+  __shared__ uint32_t acc[kAccWords];
   __shared__ uint32_t info[kBlock][4];
+  // acc[byte offset / 4] += v, through the padded layout when kSwz
+  auto add = [&](uint32_t byte_off, uint32_t v) {
+    lds_add(acc, kSwz ? byte_off + ((byte_off >> 7) << 2) : byte_off, v);
+  };
   const int t = blockIdx.x, r = blockIdx.y, g = blockIdx.z, R = gridDim.y;
   const int T = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t E0 = (uint32_t)t * kSumTile;
   const uint32_t W = min((uint32_t)kSumTile, (uint32_t)L - E0);
-  for (int i = tid; i < kSumAcc; i += kBlock) acc[i] = 0;
+  for (int i = tid; i < kAccWords; i += kBlock) acc[i] = 0;
   const int pbeg = g * Pg, pend = min(P, pbeg + Pg);
   uint32_t bad = 0;      // bit 7 / bit 0 of any byte: not a canonical short stream
   bool malformed = false;
@@ -414,8 +428,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMa
         const uint32_t total = wave_read_lane(incl, 63);
         // byte offset (within acc) of the rank of this lane's first terminator
         uint32_t a4 = 4u * (rank + kSumMargin - E0 + (incl - c));
-        if constexpr (kMaxBytes <= 2) lds_add(acc, a4, ((pm1 >> 24) & 0x7fu) & (0u - (pm1 >> 31)));
-        else lds_add(acc, a4, lead);
+        if constexpr (kMaxBytes <= 2) add(a4, ((pm1 >> 24) & 0x7fu) & (0u - (pm1 >> 31)));
+        else add(a4, lead);
         uint32_t wp = pm1;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -445,8 +459,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMa
           asm volatile("" : "+v"(ex4), "+v"(w7), "+v"(sh4));
 #pragma unroll
           for (int u = 0; u < 4; ++u)
-            lds_add(acc, a4 + ((ex4 >> (8 * u)) & 0xffu),
-                    ((w7 >> (8 * u)) & 0xffu) << ((sh4 >> (8 * u)) & 0xffu));
+            add(a4 + ((ex4 >> (8 * u)) & 0xffu), ((w7 >> (8 * u)) & 0xffu) << ((sh4 >> (8 * u)) & 0xffu));
           a4 += pre4 >> 24;
           wp = x;
         }
@@ -456,7 +469,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMa
   }
   __syncthreads();
   uint32_t* out = part + ((size_t)g * R + r) * L + E0;
-  for (uint32_t i = tid; i < W; i += kBlock) out[i] = acc[kSumMargin + i];
+  for (uint32_t i = tid; i < W; i += kBlock) {
+    const uint32_t x = kSumMargin + i;
+    out[i] = acc[kSwz ? x + (x >> 5) : x];
+  }
   if (bad) atomicOr(redo, 1u);
   if (malformed) atomicOr(err, kErrMalformed);
 }
@@ -575,6 +591,8 @@ __global__ void k_sub_mod(int D, uint32_t m, const uint32_t* __restrict__ a,
 
 static int g_decode_lean = 1;
 void set_decode_lean(int mode) { g_decode_lean = mode; }
+static int g_decode_swz = -1;  // padded accumulator rows: -1 by modulus, 0 never, 1 always
+void set_decode_swz(int mode) { g_decode_swz = mode; }
 
 void launch_decode(int M, int K, int L, uint32_t m, int value_bytes, const uint8_t* pt,
                    uint64_t stride, const uint32_t* pt_len, const uint32_t* elem_start,
@@ -611,12 +629,17 @@ void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* p
   // generic one then runs only if `redo` was raised (it rewrites every slab)
   // (codes of 2 bytes below 2^14, of 4 bytes below 2^28: moduli up to 2^13 / 2^27)
   const bool lean = g_decode_lean && redo != nullptr && m <= (1u << 27);
-  if (lean && m <= 8192u)
-    hipLaunchKernelGGL(k_decode_sum_z<2>, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S,
-                       pre, tile_sub, part, redo, err, 0);
-  else if (lean)  // canonical codes 2 (m - 1) below 2^21 have at most three bytes
-    hipLaunchKernelGGL(k_decode_sum_z<4>, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S,
-                       pre, tile_sub, part, redo, err, 2ull * (m - 1) < (1ull << 21) ? 1 : 0);
+  // padded accumulator rows where the codes are (nearly) all of one length
+  const bool swz = g_decode_swz < 0 ? m > 2048u : g_decode_swz != 0;
+  if (lean && m <= 8192u) {
+    auto kern = swz ? k_decode_sum_z<2, true> : k_decode_sum_z<2, false>;
+    hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S, pre,
+                       tile_sub, part, redo, err, 0);
+  } else if (lean) {  // canonical codes 2 (m - 1) below 2^21 have at most three bytes
+    auto kern = swz ? k_decode_sum_z<4, true> : k_decode_sum_z<4, false>;
+    hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S, pre,
+                       tile_sub, part, redo, err, 2ull * (m - 1) < (1ull << 21) ? 1 : 0);
+  }
   const uint32_t* gate = lean ? redo : nullptr;
   if (m < 65536u)
     hipLaunchKernelGGL(k_decode_sum<true>, grid, dim3(kBlock), 0, s, L, P, Pg, mp, pt, stride,

@@ -114,7 +114,11 @@ __global__ void __launch_bounds__(kBlock)
   const int tid = threadIdx.x;
   const int e0 = t * kEncodeValues + tid * kValuesPerLane;
   const VT* src = vals + (size_t)j * L;
+  // full: all 32 values present (the lane's values are then in registers); a tile's
+  // last lane with values takes the rolled loops below, straight from memory, and
+  // the lanes past the message's end (most of a short message's last tile) nothing
   const bool full = e0 + kValuesPerLane <= L;
+  const int nv = full ? kValuesPerLane : max(0, L - e0);
   uint32_t v[kValuesPerLane];            // the lane's values (u8 / u32 storage)
   uint32_t pr[kValuesPerLane / 2] = {};  // u16 storage: the lane's values as pairs, as loaded
   // Fast lanes (all 32 values present and < 2^13, i.e. 1- or 2-byte varints of
@@ -123,6 +127,7 @@ __global__ void __launch_bounds__(kBlock)
   // Middle lanes (all 32 values present and < 2^27: varints of up to four bytes, the
   // large packed-Shamir fields) encode branch-free too, 32-bit arithmetic only.
   bool mid = false;
+  bool mid3 = false;  // ... all < 2^20: at most three bytes (fields below 2^20, u16 storage)
   uint32_t my_bytes = 0;
   if constexpr (sizeof(VT) == 2) {
     // u16 pairs stay packed: both halves of a dword are handled by one
@@ -137,10 +142,6 @@ __global__ void __launch_bounds__(kBlock)
       }
 #pragma unroll
       for (int k = 0; k < kValuesPerLane / 2; ++k) orp |= pr[k];
-    } else {
-#pragma unroll
-      for (int i = 0; i < kValuesPerLane; ++i)
-        pr[i >> 1] |= ((e0 + i < L) ? (uint32_t)src[e0 + i] : 0u) << (16 * (i & 1));
     }
     fast = full && (orp & 0xe000e000u) == 0u;
     if (fast) {
@@ -149,36 +150,50 @@ __global__ void __launch_bounds__(kBlock)
       for (int k = 0; k < kValuesPerLane / 2; ++k)
         my_bytes += (uint32_t)__popc((pr[k] + 0x7fc07fc0u) & 0x80008000u);
     }
-    mid = !fast && full;
+    mid = mid3 = !fast && full;
   } else {
-    load_values<VT>(v, src, e0, L);
     uint32_t orv = 0;
+    if (full) {
+      load_values<VT>(v, src, e0, L);
 #pragma unroll
-    for (int i = 0; i < kValuesPerLane; ++i) orv |= v[i];
+      for (int i = 0; i < kValuesPerLane; ++i) orv |= v[i];
+    }
     fast = full && orv < 8192u;
     if (fast) {
 #pragma unroll
       for (int i = 0; i < kValuesPerLane; ++i) my_bytes += 1u + (v[i] >= 64u);
     }
     mid = !fast && full && orv < (1u << 27);
+    mid3 = mid && orv < (1u << 20);
   }
   // value i of the lane on the generic paths
   auto val = [&](int i) -> uint32_t {
     if constexpr (sizeof(VT) == 2) return (pr[i >> 1] >> (16 * (i & 1))) & 0xffffu;
     else return v[i];
   };
-  if (mid) {
+  if (mid3) {
+#pragma unroll
+    for (int i = 0; i < kValuesPerLane; ++i) {
+      const uint32_t z = val(i) << 1;
+      my_bytes += 1u + (z >= (1u << 7)) + (z >= (1u << 14));
+    }
+  } else if (mid) {
 #pragma unroll
     for (int i = 0; i < kValuesPerLane; ++i) {
       const uint32_t z = val(i) << 1;
       my_bytes += 1u + (z >= (1u << 7)) + (z >= (1u << 14)) + (z >= (1u << 21));
     }
-  } else if (!fast) {
+  } else if (!fast && full) {
 #pragma unroll
     for (int i = 0; i < kValuesPerLane; ++i) {
       const uint64_t z = (uint64_t)val(i) << 1;
-      const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
-      my_bytes += (e0 + i < L) ? len : 0u;
+      my_bytes += 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
+    }
+  } else if (!fast) {
+#pragma unroll 1
+    for (int i = 0; i < nv; ++i) {
+      const uint64_t z = (uint64_t)src[e0 + i] << 1;
+      my_bytes += 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
     }
   }
   uint32_t tile_bytes;
@@ -218,6 +233,17 @@ __global__ void __launch_bounds__(kBlock)
         pos += 1u + l2;
       }
     }
+  } else if (mid3) {
+    // as below, three candidate bytes
+#pragma unroll
+    for (int i = 0; i < kValuesPerLane; ++i) {
+      const uint32_t z = val(i) << 1;
+      const uint32_t l1 = z >= (1u << 7), l2 = z >= (1u << 14);
+      lds[pos] = (uint8_t)((z & 0x7fu) | (l1 << 7));
+      if (i + 1 < kValuesPerLane || l1) lds[pos + 1] = (uint8_t)(((z >> 7) & 0x7fu) | (l2 << 7));
+      if (i + 2 < kValuesPerLane || l2) lds[pos + 2] = (uint8_t)(z >> 14);
+      pos += 1u + l1 + l2;
+    }
   } else if (mid) {
     // every value stores its four candidate bytes; what lies past its length is
     // overwritten by the following values of the lane (each at least one byte), so
@@ -232,18 +258,27 @@ __global__ void __launch_bounds__(kBlock)
       if (i + 3 < kValuesPerLane || l3) lds[pos + 3] = (uint8_t)(z >> 21);
       pos += 1u + l1 + l2 + l3;
     }
-  } else {
+  } else if (full) {
 #pragma unroll
     for (int i = 0; i < kValuesPerLane; ++i) {
-      if (e0 + i < L) {
-        const uint64_t z = (uint64_t)val(i) << 1;
-        const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
+      const uint64_t z = (uint64_t)val(i) << 1;
+      const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
 #pragma unroll
-        for (int q = 0; q < 5; ++q)
-          if ((uint32_t)q < len)
-            lds[pos + q] = (uint8_t)(((z >> (7 * q)) & 0x7f) | ((uint32_t)q + 1 < len ? 0x80u : 0u));
-        pos += len;
-      }
+      for (int q = 0; q < 5; ++q)
+        if ((uint32_t)q < len)
+          lds[pos + q] = (uint8_t)(((z >> (7 * q)) & 0x7f) | ((uint32_t)q + 1 < len ? 0x80u : 0u));
+      pos += len;
+    }
+  } else {
+#pragma unroll 1
+    for (int i = 0; i < nv; ++i) {
+      const uint64_t z = (uint64_t)src[e0 + i] << 1;
+      const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
+#pragma unroll
+      for (int q = 0; q < 5; ++q)
+        if ((uint32_t)q < len)
+          lds[pos + q] = (uint8_t)(((z >> (7 * q)) & 0x7f) | ((uint32_t)q + 1 < len ? 0x80u : 0u));
+      pos += len;
     }
   }
   __syncthreads();
@@ -404,8 +439,7 @@ __global__ void __launch_bounds__(kBlock) k_segscan(int T, uint32_t* __restrict_
 
 // Read 16 ciphertext bytes as a Poly1305 block (block index i of a message of N
 // bytes at gmsg; a partial final block reads into the slot padding).
-SDA_DEV P130 load_block(const uint8_t* gmsg, int64_t i, uint32_t N) {
-  const uint4 q = *reinterpret_cast<const uint4*>(gmsg + 16 * i);
+SDA_DEV P130 block_from(const uint4 q, int64_t i, uint32_t N) {
   uint32_t w[4] = {q.x, q.y, q.z, q.w};
   uint32_t hibit = 1u << 24;
   const int64_t rem = (int64_t)N - 16 * i;
@@ -421,6 +455,9 @@ SDA_DEV P130 load_block(const uint8_t* gmsg, int64_t i, uint32_t N) {
     hibit = 0;
   }
   return p130_block(w[0], w[1], w[2], w[3], hibit);
+}
+SDA_DEV P130 load_block(const uint8_t* gmsg, int64_t i, uint32_t N) {
+  return block_from(*reinterpret_cast<const uint4*>(gmsg + 16 * i), i, N);
 }
 
 // r^(4 * (255 - t)) for t = 0..255, per message: the factor that places lane t's
@@ -703,7 +740,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     const int64_t end = min((int64_t)N, kC + kChunkBytes - 32);
     uint32_t* part = partials + ((size_t)j * K + k) * 8;
     if (start >= end) {  // chunk beyond the message (or empty message)
-      if (tid < 5) part[tid] = 0;
+      if (tid < 5 && partials != nullptr) part[tid] = 0;
       if (DECRYPT && term_cnt && tid == 0) term_cnt[(size_t)j * K + k] = 0;
       if (DECRYPT && sub_cnt && tid < kSubPerChunk)
         sub_cnt[((size_t)j * K + k) * kSubPerChunk + tid] = 0;
@@ -949,6 +986,99 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+// ------------------------------------------------ short messages: one pass --
+// Boxes of at most kShortMaxChunks chunks (the many-clerk committees seal hundreds
+// of thousands of 30-40 KB boxes) take neither the chunk tables nor the partials:
+// a wave owns a message and lane t the blocks at distance e = t + 64 i from the
+// message's last one, so that one load instruction of the wave reads 1 KiB of
+// contiguous ciphertext:
+//   tag = sum_e c_e r^(e+1) = sum_t r^(t+1) sum_i c_(t+64i) (r^64)^i,
+// a Horner chain in R = r^64 per lane, one multiply by the lane's r^(t+1), a sum
+// over the lanes, and the tag -- one multiply per block where the chunked path
+// needs 1.25 plus a 256-entry factor table per message (more multiplies than such
+// a message's own blocks) and a combining pass. The table here: r^1 .. r^64.
+__global__ void __launch_bounds__(kBlock)
+    k_poly_powers_short(int M, const MsgKey* __restrict__ keys, uint32_t* __restrict__ pows, int prio) {
+  if (prio) __builtin_amdgcn_s_setprio(3);  // side-stream key work (see k_seal_setup)
+  const int j = blockIdx.x * kWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (j >= M) return;  // wave-uniform
+  const MsgKey key = keys[j];
+  const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
+  const P130 f = p130_carry(p130_pow(p130_r_from_key(rk), (uint32_t)lane + 1u));
+  uint32_t* out = pows + (size_t)j * kPowShortWords + lane * 5;
+#pragma unroll
+  for (int u = 0; u < 5; ++u) out[u] = f.v[u];
+}
+
+template <bool VERIFY>
+__global__ void __launch_bounds__(kBlock)
+    k_mac_short(int M, const MsgKey* __restrict__ keys, const uint32_t* __restrict__ pows,
+                uint8_t* __restrict__ ct, uint64_t stride, const uint32_t* __restrict__ pt_len,
+                uint32_t* __restrict__ ok, uint32_t* err) {
+  const int j = blockIdx.x * kWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (j >= M) return;  // wave-uniform
+  const uint32_t N = pt_len[j];
+  const int nb = (int)(((int64_t)N + 15) / 16);
+  const uint8_t* gmsg = ct + (size_t)j * stride + 48;
+  const uint32_t* pw = pows + (size_t)j * kPowShortWords;
+  const P130 R = P130{{pw[63 * 5], pw[63 * 5 + 1], pw[63 * 5 + 2], pw[63 * 5 + 3], pw[63 * 5 + 4]}};
+  const P130 f = P130{{pw[lane * 5], pw[lane * 5 + 1], pw[lane * 5 + 2], pw[lane * 5 + 3], pw[lane * 5 + 4]}};
+  // rounds of 64 blocks, in groups of four whose loads are issued together (rounds
+  // past the message's first block read as zero and leave h = 0)
+  const int I4 = (((nb + 63) / 64) + 3) & ~3;
+  auto fetch = [&](int i) -> uint4 {
+    const int e = lane + 64 * i;
+    return e < nb ? *reinterpret_cast<const uint4*>(gmsg + 16 * (int64_t)(nb - 1 - e)) : make_uint4(0, 0, 0, 0);
+  };
+  auto block = [&](const uint4& q, int i) -> P130 {
+    const int e = lane + 64 * i;
+    return e < nb ? block_from(q, nb - 1 - e, N) : p130_zero();
+  };
+  P130 h = p130_zero();
+  for (int i = I4 - 1; i >= 0; i -= 4) {
+    const uint4 q0 = fetch(i), q1 = fetch(i - 1), q2 = fetch(i - 2), q3 = fetch(i - 3);
+    h = p130_mul(p130_add(h, block(q0, i)), R);
+    h = p130_mul(p130_add(h, block(q1, i - 1)), R);
+    h = p130_mul(p130_add(h, block(q2, i - 2)), R);
+    h = p130_add(h, block(q3, i - 3));
+    if (i > 3) h = p130_mul(h, R);  // wave-uniform
+  }
+  h = p130_carry(p130_mul(h, f));  // limbs <= 2^26
+  // over the lanes: rows of 16 on the VALU (16 x 2^26 fits a word), the four rows as
+  // 64-bit scalars
+  uint64_t d[5];
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const uint32_t rs = row16_incl_scan(h.v[u]);
+    d[u] = (uint64_t)wave_read_lane(rs, 15) + wave_read_lane(rs, 31) + wave_read_lane(rs, 47) +
+           wave_read_lane(rs, 63);
+  }
+  if (lane != 0) return;
+  uint64_t c;
+  c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+  c = d[1] >> 26; d[1] &= kM26; d[2] += c;
+  c = d[2] >> 26; d[2] &= kM26; d[3] += c;
+  c = d[3] >> 26; d[3] &= kM26; d[4] += c;
+  c = d[4] >> 26; d[4] &= kM26; d[0] += c * 5;
+  c = d[0] >> 26; d[0] &= kM26; d[1] += c;
+  const P130 H = P130{{(uint32_t)d[0], (uint32_t)d[1], (uint32_t)d[2], (uint32_t)d[3], (uint32_t)d[4]}};
+  const MsgKey key = keys[j];
+  const uint32_t s4[4] = {key.poly_s[0], key.poly_s[1], key.poly_s[2], key.poly_s[3]};
+  uint32_t tag[4];
+  p130_finish(tag, H, s4);
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(ct + (size_t)j * stride + 32);
+  if constexpr (!VERIFY) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) hdr[i] = tag[i];
+  } else {
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) diff |= hdr[i] ^ tag[i];
+    if (ok) ok[j] = diff == 0 ? 1u : 0u;
+    if (diff) atomicOr(err, kErrMac);
+  }
+}
+
 }  // namespace
 
 void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, uint32_t expect, uint32_t* err,
@@ -995,6 +1125,35 @@ void launch_mac_edges(int M, int K, const MsgKey* keys, const uint32_t* pows, co
   if (M <= 0 || K <= 0) return;
   hipLaunchKernelGGL(k_mac_horner, dim3(2, M), dim3(kBlock), 0, s, K, keys, pows, ct, stride, pt_len,
                      partials, 0);
+}
+
+void launch_poly_powers_short(int M, const MsgKey* keys, uint32_t* pows, hipStream_t s) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(k_poly_powers_short, dim3((M + kWaves - 1) / kWaves), dim3(kBlock), 0, s, M, keys,
+                     pows, g_powers_prio);
+}
+
+void launch_mac_short(int M, const MsgKey* keys, const uint32_t* pows, uint8_t* ct, uint64_t stride,
+                      const uint32_t* pt_len, int verify, uint32_t* ok, uint32_t* err, hipStream_t s) {
+  if (M <= 0) return;
+  const dim3 grid((M + kWaves - 1) / kWaves);
+  if (verify)
+    hipLaunchKernelGGL(k_mac_short<true>, grid, dim3(kBlock), 0, s, M, keys, pows, ct, stride, pt_len,
+                       ok, err);
+  else
+    hipLaunchKernelGGL(k_mac_short<false>, grid, dim3(kBlock), 0, s, M, keys, pows, ct, stride, pt_len,
+                       ok, err);
+}
+
+void launch_decrypt_count(int M, int K, const MsgKey* keys, uint8_t* ct, uint64_t stride,
+                          const uint32_t* pt_len, uint32_t* term_cnt, uint32_t* sub_cnt,
+                          hipStream_t s) {
+  if (M <= 0 || K <= 0) return;
+  int cpb = kMacChunksPerBlock;
+  while (cpb > 1 && (int64_t)M * ((K + cpb - 1) / cpb) < 16384) cpb /= 2;
+  const dim3 grid((K + cpb - 1) / cpb, M);
+  hipLaunchKernelGGL((k_mac_chunks<1, false>), grid, dim3(kBlock), 0, s, K, keys, nullptr, ct, stride,
+                     pt_len, nullptr, term_cnt, sub_cnt, 0, cpb);
 }
 
 static int g_mac_mfma = 1;

@@ -221,9 +221,10 @@ class DeviceAggregator:
                 masked = G.mask_secrets(secrets, m, rng_key, owner_base, mask_vals, mask_cnt)
             ps = spec.sharing
             X = G.pss_x_limbs(masked, ps.secret_count, ps.privacy_threshold_, m, rng_key, owner_base)
+            cnt.zero_()  # the GEMM epilogue adds the boxes' varint bytes into it
             G.modgemm_i8(self._M_limbs, X, m, shares, ldc_z=B, ldc_m=P * B, ldc_n=1,
-                         limit=n * P * B)
-            return shares, None, mask_vals, mask_cnt
+                         limit=n * P * B, cnt=cnt)
+            return shares, cnt, mask_vals, mask_cnt
         mode = G.MASK_FULL if full else G.MASK_NONE
         if self._pss is None:
             G.share_additive(secrets, n, m, shares, cnt, mode, rng_key, owner_base,

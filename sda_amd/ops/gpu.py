@@ -17,6 +17,8 @@ SUB_PER_CHUNK = CHUNK_BYTES // SUB_BYTES
 SUM_TILE = 6144                   # elements per decode-sum tile (k_decode_sum)
 MSGKEY_BYTES = 80
 POW_WORDS = 6560  # Poly1305 tables per message (k_poly_powers; kernels.hpp kPowWords)
+POW_SHORT_WORDS = 320  # ... of the one-pass MAC of short messages (kPowShortWords)
+SHORT_MAX_CHUNKS = 4   # messages of at most this many 16 KiB chunks take it (kShortMaxChunks)
 SEAL_OVERHEAD = 48
 
 MASK_NONE, MASK_FULL, MASK_CHACHA = 0, 1, 2
@@ -294,6 +296,47 @@ def poly_powers(M, keys, pows, full=True):
     _gpu().poly_powers(M, _ptr(keys), _ptr(pows), 1 if full else 0, _stream())
 
 
+def poly_powers_short(M, keys, pows):
+    """r^1 .. r^64 per message: the table of :func:`mac_short`."""
+    _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
+    _check(pows, "pows", torch.int32, min_numel=M * POW_SHORT_WORDS)
+    _gpu().poly_powers_short(M, _ptr(keys), _ptr(pows), _stream())
+
+
+def mac_short(M, keys, pows, ct, stride, pt_len, verify, ok=None, err=None):
+    """Poly1305 of every message in one pass, a wave per message (meant for messages
+    of at most SHORT_MAX_CHUNKS chunks): writes the tag into the slot header, or
+    with `verify` compares it (`ok` [M] optional; a mismatch raises the MAC bit of
+    `err`). Reads the ciphertext, so it goes ahead of :func:`decrypt_count`."""
+    _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
+    _check(pows, "pows", torch.int32, min_numel=M * POW_SHORT_WORDS)
+    _check(ct, "ct", torch.uint8, min_numel=M * stride)
+    _check(pt_len, "pt_len", torch.int32, numel=M)
+    _check(err, "err", torch.int32, numel=1)
+    if ok is not None:
+        _check(ok, "ok", torch.int32, numel=M)
+    _gpu().mac_short(M, _ptr(keys), _ptr(pows), _ptr(ct), stride, _ptr(pt_len), 1 if verify else 0,
+                     _ptr(ok) if ok is not None else 0, _ptr(err), _stream())
+
+
+def decrypt_count(M, K, keys, ct, stride, pt_len, term_cnt=None, sub_cnt=None):
+    """In-place decryption plus varint terminator counts (per 16 KiB chunk and/or
+    per 1 KiB sub-chunk), without any MAC work: the second half of opening short
+    messages, after :func:`mac_short` has read the ciphertext."""
+    _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
+    _check(ct, "ct", torch.uint8, min_numel=M * stride)
+    _check(pt_len, "pt_len", torch.int32, numel=M)
+    if term_cnt is None and sub_cnt is None:
+        raise ValueError("decrypt_count needs term_cnt and/or sub_cnt")
+    if term_cnt is not None:
+        _check(term_cnt, "term_cnt", torch.int32, numel=M * K)
+    if sub_cnt is not None:
+        _check(sub_cnt, "sub_cnt", torch.int32, numel=M * K * SUB_PER_CHUNK)
+    _gpu().decrypt_count(M, K, _ptr(keys), _ptr(ct), stride, _ptr(pt_len),
+                         _ptr(term_cnt) if term_cnt is not None else 0,
+                         _ptr(sub_cnt) if sub_cnt is not None else 0, _stream())
+
+
 def mac_edges(M, K, keys, pows, ct, stride, pt_len, partials):
     """Poly1305 partials of every message's first and last chunk (Horner)."""
     _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
@@ -459,8 +502,12 @@ def limbs_of(values: torch.Tensor, Kp: int, limbs: int) -> torch.Tensor:
 
 
 def modgemm_i8(A_limbs: torch.Tensor, B_limbs: torch.Tensor, prime: int, out: torch.Tensor,
-               ldc_z: int, ldc_m: int, ldc_n: int, limit: int):
-    """out[z*ldc_z + m*ldc_m + n*ldc_n] = (A . B_z)[m][n] mod prime (A [L][M][Kp], B [L][Z][N][Kp])."""
+               ldc_z: int, ldc_m: int, ldc_n: int, limit: int, cnt: torch.Tensor | None = None):
+    """out[z*ldc_z + m*ldc_m + n*ldc_n] = (A . B_z)[m][n] mod prime (A [L][M][Kp], B [L][Z][N][Kp]).
+
+    `cnt` (int32 [M * Z * tiles(N)], zeroed): the epilogue also adds up the varint
+    bytes of what it writes, per (row m, batch z, 4096-column tile) -- :func:`count`
+    of the output taken as M x Z messages of N values, without the extra pass."""
     _check(A_limbs, "A_limbs", torch.int8)
     _check(B_limbs, "B_limbs", torch.int8)
     L, M, Kp = A_limbs.shape
@@ -473,8 +520,13 @@ def modgemm_i8(A_limbs: torch.Tensor, B_limbs: torch.Tensor, prime: int, out: to
     max_idx = (Z - 1) * ldc_z + (M - 1) * ldc_m + (N - 1) * ldc_n
     if min(limit, max_idx + 1) > out.numel():
         raise ValueError("output too small for the GEMM index map")
+    if cnt is not None:
+        _check(cnt, "cnt", torch.int32)
+        if cnt.numel() < M * Z * tiles(N):
+            raise ValueError("cnt too small")
     _gpu().modgemm_i8(M, N, Kp, Z, L, prime, _ptr(A_limbs), _ptr(B_limbs), Z * N * Kp, vb,
-                      _ptr(out), ldc_z, ldc_m, ldc_n, limit, _stream())
+                      _ptr(out), ldc_z, ldc_m, ldc_n, limit, 0 if cnt is None else _ptr(cnt),
+                      _stream())
 
 
 def pss_x_limbs(secrets: torch.Tensor, k: int, t: int, prime: int, rng_key: bytes,

@@ -87,49 +87,64 @@ class Arena:
 @dataclass
 class KeySet:
     """Per-message derived keys: the 80-byte `MsgKey` records (XSalsa20 subkey,
-    nonce tail, Poly1305 r/s) and each message's Poly1305 tables (chunk factors
-    r^(4(255-t)) plus the weight digits, row factors and pad-bit prefixes of the
-    matrix-core MAC). Both depend only on the key agreement, so they are
-    produced together on the side stream."""
+    nonce tail, Poly1305 r/s) and each message's Poly1305 tables. Both depend only
+    on the key agreement, so they are produced together on the side stream.
+
+    Two table forms: messages of at most ``SHORT_MAX_CHUNKS`` chunks take the
+    one-pass MAC, whose table is r^1 .. r^64 (1.3 KB per message); longer ones the
+    chunked MAC with its 26 KB per message (chunk factors plus the weight digits, row
+    factors and pad-bit prefixes of the matrix-core rows)."""
     M: int
     keys: torch.Tensor  # uint8 [M * MSGKEY_BYTES]
-    pows: torch.Tensor | None  # int32 [M * POW_WORDS]; None = not derived yet
+    pows: torch.Tensor | None  # int32 [M * pow_words]; None = not derived yet
     K: int | None = None  # 16 KiB chunks per slot of the arena the keys were made for, if known
-    full: bool = True     # pows holds the matrix-core tables too (not only the Horner factors)
+    short: bool = False   # pows is the one-pass table
+
+    @property
+    def pow_words(self) -> int:
+        return G.POW_SHORT_WORDS if self.short else G.POW_WORDS
 
     @classmethod
     def derive(cls, M: int, keys: torch.Tensor, K: int | None = None) -> "KeySet":
         return cls(M, keys, None, K).with_powers()
 
     def with_powers(self) -> "KeySet":
-        """The Poly1305 tables (on the current stream) if not derived yet. Slots of at
-        most two chunks hold no middle chunk: only the Horner factors are made."""
+        """The Poly1305 tables (on the current stream) if not derived yet: the short
+        form when the slots are known to hold at most SHORT_MAX_CHUNKS chunks."""
         if self.pows is not None:
             return self
-        pows = torch.empty(self.M * G.POW_WORDS, dtype=torch.int32, device=self.keys.device)
-        full = self.K is None or self.K > 2
-        G.poly_powers(self.M, self.keys, pows, full=full)
-        return KeySet(self.M, self.keys, pows, self.K, full)
+        short = self.K is not None and self.K <= G.SHORT_MAX_CHUNKS
+        return self._tables(short)
+
+    def _tables(self, short: bool) -> "KeySet":
+        words = G.POW_SHORT_WORDS if short else G.POW_WORDS
+        pows = torch.empty(self.M * words, dtype=torch.int32, device=self.keys.device)
+        if short:
+            G.poly_powers_short(self.M, self.keys, pows)
+        else:
+            G.poly_powers(self.M, self.keys, pows, full=True)
+        return KeySet(self.M, self.keys, pows, self.K, short)
 
     def fit(self, arena: "Arena") -> "KeySet":
         """The key set ready for `arena`'s messages: same message count, and the
-        complete tables if the arena's slots can hold a middle chunk (a set made for
-        short slots gets them now, on the current stream)."""
+        chunked tables if the arena's slots are longer than the short form covers (a
+        set made for short slots gets them now, on the current stream)."""
         if self.M != arena.M:
             raise ValueError("key set does not match the arena")
-        if self.pows is not None and not self.full and arena.K > 2:
-            G.poly_powers(self.M, self.keys, self.pows, full=True)
-            self.full = True
+        if self.pows is None:
+            return KeySet(self.M, self.keys, None, arena.K).with_powers()
+        if self.short and arena.K > G.SHORT_MAX_CHUNKS:
+            return KeySet(self.M, self.keys, None, arena.K)._tables(False)
         return self
 
     def slice(self, first: int, count: int) -> "KeySet":
         """Keys of messages [first, first+count) (no copy)."""
         if first < 0 or first + count > self.M:
             raise ValueError("key slice out of range")
-        kb, pw = G.MSGKEY_BYTES, G.POW_WORDS
+        kb, pw = G.MSGKEY_BYTES, self.pow_words
         return KeySet(count, self.keys[first * kb:(first + count) * kb],
                       None if self.pows is None else self.pows[first * pw:(first + count) * pw],
-                      self.K, self.full)
+                      self.K, self.short)
 
     def record_stream(self, stream) -> None:
         self.keys.record_stream(stream)
@@ -178,9 +193,9 @@ def seal_encode(arena: Arena, keys: KeySet, values: torch.Tensor,
     else:
         cnt = cnt.view(M, T)
     G.segscan(cnt, arena.pt_len)  # cnt becomes the tile byte offsets
-    keys = keys.with_powers().fit(arena)
+    keys = keys.fit(arena)
     partials = None
-    if FUSED_SEAL_MAC:
+    if FUSED_SEAL_MAC and not keys.short:
         # one pass: every tile adds its share of the middle chunks' Poly1305 partials
         # while its ciphertext is in LDS; the first / last chunks follow by Horner
         partials = torch.zeros(M * arena.K * 8, dtype=torch.int32, device=dev)
@@ -196,6 +211,10 @@ def seal_mac(arena: Arena, keys: KeySet, partials, err: torch.Tensor) -> Arena:
     header. Reads the stored ciphertext (all of it, or only the first and last
     chunk of every message when the encode pass already did the middle ones)."""
     M, dev = arena.M, arena.ct.device
+    if keys.short:
+        G.mac_short(M, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, verify=False,
+                    err=err)
+        return arena
     if partials is not None:
         G.mac_edges(M, arena.K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials)
     else:
@@ -205,6 +224,23 @@ def seal_mac(arena: Arena, keys: KeySet, partials, err: torch.Tensor) -> Arena:
     G.mac_final(M, arena.K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials, verify=False,
                 err=err)
     return arena
+
+
+def _verify_decrypt(arena: Arena, keys: KeySet, err: torch.Tensor, term_cnt=None, sub_cnt=None):
+    """Check every box's tag, then decrypt in place and count varint terminators
+    (per chunk and/or per 1 KiB sub-chunk)."""
+    M, K = arena.M, arena.K
+    if keys.short:
+        G.mac_short(M, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, verify=True,
+                    err=err)
+        G.decrypt_count(M, K, keys.keys, arena.ct, arena.stride, arena.pt_len, term_cnt=term_cnt,
+                        sub_cnt=sub_cnt)
+        return
+    partials = torch.empty(M * K * 8, dtype=torch.int32, device=arena.ct.device)
+    G.mac_chunks(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
+                 decrypt=True, term_cnt=term_cnt, sub_cnt=sub_cnt)
+    G.mac_final(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
+                verify=True, err=err)
 
 
 def seal_data(arena: Arena, keys: KeySet, values: torch.Tensor, err: torch.Tensor,
@@ -242,11 +278,8 @@ def open_data(arena: Arena, keys: KeySet, err: torch.Tensor,
     M, L, K = arena.M, arena.L, arena.K
     dev = arena.ct.device
     keys = keys.fit(arena)
-    partials = torch.empty(M * K * 8, dtype=torch.int32, device=dev)
     term = torch.empty(M, K, dtype=torch.int32, device=dev)
-    G.mac_chunks(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
-                 decrypt=True, term_cnt=term)
-    G.mac_final(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials, verify=True, err=err)
+    _verify_decrypt(arena, keys, err, term_cnt=term)
     totals = torch.empty(M, dtype=torch.int32, device=dev)
     G.segscan(term, totals, expect=L, err=err)  # exactly L values per message, else malformed
     if out is None:
@@ -290,11 +323,8 @@ def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
     P = M // rows
     dev = arena.ct.device
     S = K * G.SUB_PER_CHUNK
-    partials = torch.empty(M * K * 8, dtype=torch.int32, device=dev)
     pre = torch.empty(M, S, dtype=torch.int32, device=dev)
-    G.mac_chunks(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials,
-                 decrypt=True, sub_cnt=pre)
-    G.mac_final(M, K, keys.keys, keys.pows, arena.ct, arena.stride, arena.pt_len, partials, verify=True, err=err)
+    _verify_decrypt(arena, keys, err, sub_cnt=pre)
     totals = torch.empty(M, dtype=torch.int32, device=dev)
     # sub-chunk counts -> exclusive ranks; exactly L values per message, else malformed
     G.segscan(pre, totals, expect=L, err=err)

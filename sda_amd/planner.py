@@ -34,6 +34,8 @@ SUB_PER_CHUNK = 16
 SUM_TILE = 6144
 MSGKEY_BYTES = 80
 POW_WORDS = 6560
+POW_SHORT_WORDS = 320   # boxes of at most SHORT_MAX_CHUNKS chunks: the one-pass MAC's table
+SHORT_MAX_CHUNKS = 4
 SEAL_OVERHEAD = 48
 
 HBM_BYTES_MI355X = 288 * 10 ** 9
@@ -69,9 +71,11 @@ def _box_bytes(L: int, modulus: int, opened: bool) -> int:
     """One sealed box of L values: slot, stream key + Poly1305 tables, MAC partials
     and (when it is opened here) the terminator counts of the decode."""
     K = chunks_for(L * varint_max_len(modulus))
-    b = slot_stride(L, modulus) + MSGKEY_BYTES + POW_WORDS * 4 + K * 32 + 4
+    short = K <= SHORT_MAX_CHUNKS
+    tables = (POW_SHORT_WORDS if short else POW_WORDS) * 4 + (0 if short else K * 32)
+    b = slot_stride(L, modulus) + MSGKEY_BYTES + tables + 4
     if opened:
-        b += MSGKEY_BYTES + POW_WORDS * 4 + K * 32 + K * SUB_PER_CHUNK * 4 + 8 + \
+        b += MSGKEY_BYTES + tables + K * SUB_PER_CHUNK * 4 + 8 + \
             ((L + SUM_TILE - 1) // SUM_TILE + 1) * 4
     return b
 

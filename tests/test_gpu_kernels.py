@@ -116,6 +116,46 @@ def test_mac_modes_seal_and_open(cuda, native, mode):
         gpu().set_mac_mfma(1)
 
 
+def test_one_pass_mac_block_edges(cuda, native):
+    """Boxes of at most four chunks take the one-pass MAC (a wave per message, lanes
+    strided over the 16-byte blocks from the message's end): plaintext lengths
+    around every edge of that layout -- partial and whole final blocks, one block
+    short of / exactly / one past a round of 64 blocks and a group of four rounds,
+    the longest short box and the first chunked one (an arena sized for two-byte
+    codes switches at L = 32752, one built from the blobs at 65504 bytes) -- sealed on
+    the GPU and opened on the host, and sealed on the host and opened on the GPU.
+    One-byte codes, so a box of L values has L plaintext bytes."""
+    from sda_amd.ops import gpu as G
+    from sda_amd.ops.sealed import Arena, open_, seal
+    m = 433
+    keys = _keytable(native, cuda, 1)
+    kidx = torch.zeros(2, dtype=torch.int32, device=cuda)
+    for L in (1, 15, 16, 17, 1007, 1008, 1009, 1023, 1024, 1025, 4095, 4096, 4097, 4112, 8191,
+              16352, 16353, 32752, 32753, 65504, 65505):
+        vals64 = torch.randint(0, 64, (2, L), dtype=torch.int64)
+        err = torch.zeros(1, dtype=torch.int32, device=cuda)
+        arena = seal(vals64.to(torch.int16).to(cuda), kidx, keys.pks, os.urandom(32), 0, err, m)
+        blobs = arena.to_blobs()
+        assert int(err.item()) == 0
+        for j in range(2):
+            assert len(blobs[j]) == 48 + L
+            pt = native.crypto.box_seal_open(blobs[j], keys.pk_bytes[0], keys.sk_bytes[0])
+            assert pt is not None and varint_decode(pt) == vals64[j].tolist(), (L, j)
+        host = [native.crypto.box_seal(varint_encode(vals64[j].tolist()), keys.pk_bytes[0])
+                for j in range(2)]
+        back = Arena.from_blobs(host, L, m, cuda)
+        out = open_(back, kidx, keys.sks, keys.pks, err, out_dtype=torch.int32)
+        assert int(err.item()) == 0, L
+        assert torch.equal(out.cpu().to(torch.int64), vals64), L
+        # a flipped bit anywhere fails the check: first, middle and last byte
+        for pos in (48, 48 + L // 2, 48 + L - 1, 33):
+            bad = bytearray(host[0])
+            bad[pos] ^= 0x40
+            e2 = torch.zeros(1, dtype=torch.int32, device=cuda)
+            open_(Arena.from_blobs([bytes(bad), host[1]], L, m, cuda), kidx, keys.sks, keys.pks, e2)
+            assert int(e2.item()) & 2, (L, pos)
+
+
 def _open_sum_case(native, cuda, rows_, P, L, m, gen):
     """Host-sealed boxes (row-major: message r*P + p) -> open_sum vs a plain sum."""
     from sda_amd.ops.sealed import Arena, open_setup, open_sum
@@ -186,6 +226,29 @@ def test_open_sum_canonical_streams(cuda, native, L, m, lean):
         e, out, ref = _open_sum_case(native, cuda, 2, 11, L, m, gen)
     finally:
         gpu().set_decode_lean(1)
+    assert e == 0
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("swz", [0, 1])
+@pytest.mark.parametrize("L,m", [(6145, 433), (20000, 433), (30000, 8191), (20000, 746497),
+                                 (20000, 5038849)])
+def test_open_sum_accumulator_layouts(cuda, native, L, m, swz):
+    """The lean decode-sum kernels with plain and with padded (33-word) accumulator
+    rows, each forced for every modulus: both equal the plain sum."""
+    from sda_amd._native import gpu
+
+    def gen(j):
+        if j % 3 == 0:
+            return torch.randint(min(64, m - 1), m, (L,)).tolist()
+        if j % 3 == 1:
+            return [(m - 1) if (i % 5) else 0 for i in range(L)]
+        return torch.randint(0, m, (L,)).tolist()
+    gpu().set_decode_swz(swz)
+    try:
+        e, out, ref = _open_sum_case(native, cuda, 2, 9, L, m, gen)
+    finally:
+        gpu().set_decode_swz(-1)
     assert e == 0
     assert torch.equal(out, ref)
 

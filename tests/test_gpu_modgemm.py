@@ -10,10 +10,15 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("prime", [746497, 5038849, 433])
+@pytest.mark.parametrize("prime,fold24", [(746497, 1), (746497, 0), (5038849, 1), (5038849, 0),
+                                          (433, 1), (16777213, 1), ((1 << 27) - 39, 1)])
 @pytest.mark.parametrize("M,N,K,Z", [(37, 45, 100, 2), (64, 64, 64, 1), (5, 300, 255, 3),
                                      (130, 17, 700, 1)])
-def test_modgemm_matches_torch(cuda, prime, M, N, K, Z):
+def test_modgemm_matches_torch(cuda, prime, fold24, M, N, K, Z):
+    """Every epilogue: the Horner fold on the 24-bit multipliers (2^16 <= p < 2^24),
+    the same with 32-bit Barrett steps (forced, and for small p), and the 64-bit fold
+    (p >= 2^24)."""
+    from sda_amd._native import gpu
     from sda_amd.ops import gpu as G
 
     g = torch.Generator().manual_seed(M * N + K)
@@ -24,8 +29,12 @@ def test_modgemm_matches_torch(cuda, prime, M, N, K, Z):
     Al = G.limbs_of(A.to(torch.int32).cuda(), Kp, L)
     Bl = torch.stack([G.limbs_of(Bm[z].to(torch.int32).cuda(), Kp, L) for z in range(Z)], 1)
     out = torch.zeros(Z * M * N, dtype=torch.int32, device="cuda")
-    G.modgemm_i8(Al.contiguous(), Bl.contiguous(), prime, out, ldc_z=M * N, ldc_m=N, ldc_n=1,
-                 limit=Z * M * N)
+    gpu().set_gemm_fold24(fold24)
+    try:
+        G.modgemm_i8(Al.contiguous(), Bl.contiguous(), prime, out, ldc_z=M * N, ldc_m=N, ldc_n=1,
+                     limit=Z * M * N)
+    finally:
+        gpu().set_gemm_fold24(1)
     # exact reference: split K to keep int64 products exact
     ref = torch.stack([(A @ Bm[z].T) % prime for z in range(Z)]) if prime < 2 ** 21 else \
         torch.stack([sum((A[:, i:i + 1] * Bm[z][:, i:i + 1].T) % prime for i in range(K)) % prime
@@ -48,6 +57,37 @@ def test_modgemm_transposed_truncated_store(cuda):
                  limit=D)
     ref = ((Lm @ Y) % p).T.reshape(-1)[:D]
     assert torch.equal(out.cpu().to(torch.int64), ref)
+
+
+@pytest.mark.parametrize("prime,dtype", [(746497, torch.int32), (5038849, torch.int32),
+                                         (433, torch.int16), (60013, torch.int16)])
+@pytest.mark.parametrize("M,N,Z", [(37, 45, 2), (70, 4096 + 300, 3), (9, 9000, 1)])
+def test_modgemm_epilogue_counts_varint_bytes(cuda, prime, dtype, M, N, Z):
+    """The share layout (C[m][z][n]) with `cnt`: the epilogue's byte counts per
+    (row, batch, 4096-column tile) equal the counting kernel's over the stored output."""
+    from sda_amd.ops import gpu as G
+
+    K = 130
+    g = torch.Generator().manual_seed(N + Z)
+    A = torch.randint(0, prime, (M, K), generator=g, dtype=torch.int64)
+    Bm = torch.randint(0, prime, (Z, N, K), generator=g, dtype=torch.int64)
+    Bm[:, ::5] = 0  # short codes too: whole output columns of zeros
+    L = G.limb_count(prime)
+    Kp = G.padded_k(K)
+    Al = G.limbs_of(A.to(torch.int32).cuda(), Kp, L)
+    Bl = torch.stack([G.limbs_of(Bm[z].to(torch.int32).cuda(), Kp, L) for z in range(Z)], 1)
+    out = torch.zeros(M, Z, N, dtype=dtype, device="cuda")
+    T = G.tiles(N)
+    cnt = torch.zeros(M * Z * T, dtype=torch.int32, device="cuda")
+    G.modgemm_i8(Al.contiguous(), Bl.contiguous(), prime, out, ldc_z=N, ldc_m=Z * N, ldc_n=1,
+                 limit=M * Z * N, cnt=cnt)
+    ref = torch.empty(M * Z, T, dtype=torch.int32, device="cuda")
+    G.count(out.view(M * Z, N), ref)
+    assert torch.equal(cnt.view(M * Z, T), ref)
+    v = out.cpu().to(torch.int64) & (0xFFFF if dtype == torch.int16 else 0xFFFFFFFF)
+    z2 = 2 * v
+    lens = 1 + (z2 >= 1 << 7).long() + (z2 >= 1 << 14).long() + (z2 >= 1 << 21).long() + (z2 >= 1 << 28).long()
+    assert int(lens.sum()) == int(cnt.sum())
 
 
 def _round(spec, P, clerks=None, **kw):

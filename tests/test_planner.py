@@ -59,13 +59,13 @@ def test_config4_streams_and_fills_the_card(native):
 
 def test_many_clerk_configs(native):
     c6 = _plan(6, HBM_BYTES_MI355X)     # 728 clerks: resident on 288 GB ...
-    assert c6.resident and c6.planned_bytes > 100 * GB
+    assert c6.resident and c6.planned_bytes > 80 * GB
     c6s = _plan(6, 64 * GB)             # ... in waves on 64 GB
-    assert not c6s.resident and c6s.wave == 320
+    assert not c6s.resident and c6s.wave == 592
     c8 = _plan(8, HBM_BYTES_MI355X)     # 19,682 clerks x 16 participants
     assert c8.resident
-    c8s = _plan(8, 64 * GB)
-    assert not c8s.resident and c8s.wave == 10
+    c8s = _plan(8, 32 * GB)
+    assert not c8s.resident and c8s.wave == 8
 
 
 def test_larger_rounds_stream_instead_of_failing(native):
