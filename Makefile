@@ -74,7 +74,7 @@ $(BIN)/%: csrc/bin/%.cc $(CORE_LIB)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) $(INCS) $< $(CORE_LIB) -o $@ -pthread -ldl
 
-$(BUILD)/hip/%.o: csrc/kernels/%.hip $(wildcard csrc/kernels/*.hpp) $(wildcard csrc/include/sda/*.hpp)
+$(BUILD)/hip/%.o: csrc/kernels/%.hip $(wildcard csrc/kernels/*.hpp) $(wildcard csrc/kernels/*.inc) $(wildcard csrc/include/sda/*.hpp)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) $(INCS) -c $< -o $@
 
@@ -126,7 +126,7 @@ check: all
 # host emulation of the device algorithms (no GPU needed)
 emul: $(BUILD)/hip/host_emul
 	$(BUILD)/hip/host_emul
-$(BUILD)/hip/host_emul: csrc/kernels/host_emul.cpp $(wildcard csrc/kernels/*.hpp) $(CORE_LIB)
+$(BUILD)/hip/host_emul: csrc/kernels/host_emul.cpp $(wildcard csrc/kernels/*.hpp) csrc/kernels/ed25519_base.inc $(CORE_LIB)
 	@mkdir -p $(dir $@)
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(GPU_ARCH) $(NO_PK_F32) $(INCS) -c $< -o $@.o
 	$(HIPCC) --offload-arch=$(GPU_ARCH) $@.o $(CORE_LIB) -o $@ -pthread -ldl

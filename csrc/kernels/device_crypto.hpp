@@ -723,6 +723,122 @@ SDA_DEV void x25519(uint32_t (&out)[8], const uint32_t (&scalar)[8], const uint3
   fe10_to_words(out, fe10_mul(x2, fe10_invert(z2)));
 }
 
+// ---- fixed-base: X25519(scalar, 9) from a table of edwards25519 multiples ----
+// A sealed box's ephemeral public key is esk . 9, always the same point: with the
+// table of (j + 1) 256^i B (i < 32, j < 8; scripts/gen_ed25519_base.py) the scalar's
+// 64 signed radix-16 digits cost 64 mixed additions and 4 doublings -- about 500 field
+// multiplications against the ladder's 2,500 -- and the Montgomery u-coordinate is
+// (Z + Y) / (Z - Y) (the route of libsodium's crypto_scalarmult_base). Lanes index the
+// table by their own secret digits: there is no cache-timing observer on the device
+// worth the constant-time scan of eight entries per addition.
+constexpr int kEdEntryWords = 32;  // y+x, y-x, 2dxy: 3 x 10 limbs, padded
+struct GeP3 {
+  Fe10 X, Y, Z, T;
+};
+struct GeP1 {  // "completed" point: (X : Z) x (Y : T)
+  Fe10 X, Y, Z, T;
+};
+SDA_DEV GeP3 ge_p1_to_p3(const GeP1& r) {
+  return GeP3{fe10_mul(r.X, r.T), fe10_mul(r.Y, r.Z), fe10_mul(r.Z, r.T), fe10_mul(r.X, r.Y)};
+}
+// p + (sign ? -q : q) for the table entry q = (y+x, y-x, 2dxy) at `e`
+SDA_DEV GeP1 ge_madd(const GeP3& p, const uint32_t* e, bool neg) {
+  Fe10 ypx, ymx, xy2d;
+  const uint4* e4 = reinterpret_cast<const uint4*>(e);
+  uint32_t w[kEdEntryWords];
+#pragma unroll
+  for (int i = 0; i < kEdEntryWords / 4; ++i) {
+    const uint4 q = e4[i];
+    w[4 * i] = q.x; w[4 * i + 1] = q.y; w[4 * i + 2] = q.z; w[4 * i + 3] = q.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    ypx.v[i] = neg ? w[10 + i] : w[i];
+    ymx.v[i] = neg ? w[i] : w[10 + i];
+    xy2d.v[i] = w[20 + i];
+  }
+  if (neg) xy2d = fe10_sub_nc(fe10_set(0), xy2d);  // 2p - x: a product operand
+  GeP1 r;
+  const Fe10 a = fe10_mul(fe10_add_nc(p.Y, p.X), ypx);
+  const Fe10 b = fe10_mul(fe10_sub_nc(p.Y, p.X), ymx);
+  const Fe10 c = fe10_mul(xy2d, p.T);
+  const Fe10 d = fe10_add(p.Z, p.Z);
+  r.X = fe10_sub_nc(a, b);
+  r.Y = fe10_add_nc(a, b);
+  r.Z = fe10_add(d, c);
+  r.T = fe10_sub(d, c);
+  return r;
+}
+// 2 (X : Y : Z) as a completed point
+SDA_DEV GeP1 ge_dbl(const Fe10& X, const Fe10& Y, const Fe10& Z) {
+  const Fe10 xx = fe10_sq(X), yy = fe10_sq(Y);
+  const Fe10 zz = fe10_sq(Z);
+  const Fe10 b = fe10_add(zz, zz);
+  const Fe10 a = fe10_sq(fe10_add_nc(X, Y));
+  GeP1 r;
+  r.Y = fe10_add(yy, xx);
+  r.Z = fe10_sub(yy, xx);
+  r.X = fe10_sub(a, r.Y);
+  r.T = fe10_sub(b, r.Z);
+  return r;
+}
+SDA_DEV void x25519_base(uint32_t (&out)[8], const uint32_t (&scalar)[8], const uint32_t* table) {
+  uint32_t k[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) k[i] = scalar[i];
+  k[0] &= 0xfffffff8u;
+  k[7] &= 0x7fffffffu;
+  k[7] |= 0x40000000u;
+  // signed radix-16 digits, -8 <= e_i < 8 (the top one <= 8): nibble + carry, eight
+  // per word, kept packed as biased bytes (digit + 8)
+  uint32_t dig[16];  // four digits per word
+  {
+    uint32_t carry = 0;
+#pragma unroll
+    for (int wi = 0; wi < 8; ++wi) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        uint32_t v = ((k[wi] >> (4 * n)) & 15u) + carry;
+        carry = (v + 8u) >> 4;
+        if (wi == 7 && n == 7) carry = 0;  // the last digit keeps its carry (<= 8)
+        v = v - (carry << 4) + 8u;         // biased: 0 .. 16
+        if (n < 4) lo |= v << (8 * n); else hi |= v << (8 * (n - 4));
+      }
+      dig[2 * wi] = lo;
+      dig[2 * wi + 1] = hi;
+    }
+  }
+  auto digit = [&](int i) -> int {  // i < 64
+    uint32_t w = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) w = (i >> 2) == q ? dig[q] : w;
+    return (int)((w >> (8 * (i & 3))) & 0xffu) - 8;
+  };
+  GeP3 h{fe10_set(0), fe10_set(1), fe10_set(1), fe10_set(0)};
+  auto step = [&](int i) {
+    const int e = digit(i);
+    if (e == 0) return;  // + identity
+    const int mag = e < 0 ? -e : e;
+    h = ge_p1_to_p3(ge_madd(h, table + ((size_t)(i >> 1) * 8 + (mag - 1)) * kEdEntryWords, e < 0));
+  };
+#pragma unroll 1
+  for (int i = 1; i < 64; i += 2) step(i);
+  // h <- 16 h
+  GeP1 r = ge_dbl(h.X, h.Y, h.Z);
+#pragma unroll 1
+  for (int q = 0; q < 3; ++q) {
+    const Fe10 x = fe10_mul(r.X, r.T), y = fe10_mul(r.Y, r.Z), z = fe10_mul(r.Z, r.T);
+    r = ge_dbl(x, y, z);
+  }
+  h = ge_p1_to_p3(r);
+#pragma unroll 1
+  for (int i = 0; i < 64; i += 2) step(i);
+  const Fe10 num = fe10_add_nc(h.Z, h.Y);
+  const Fe10 den = fe10_sub(h.Z, h.Y);
+  fe10_to_words(out, fe10_mul(num, fe10_invert(den)));
+}
+
 // ------------------------------------------------------------------ varint --
 // zigzag(LEB128) length of a canonical value v in [0, 2^31): z = 2v.
 SDA_DEV uint32_t varint_len_canon(uint32_t v) {

@@ -251,7 +251,12 @@ PYBIND11_MODULE(_sda_gpu, m) {
   });
   m.def("set_decode_lean", &set_decode_lean);
   m.def("set_decode_swz", &set_decode_swz);
-  m.def("set_gemm_fold24", &set_gemm_fold24);
+  m.def("set_seal_many", &set_seal_many);
+  m.def("x25519_base", [](int N, uintptr_t sc, uintptr_t out, uintptr_t stream) {
+    launch_x25519_base(N, P<const uint32_t>(sc), P<uint32_t>(out), S(stream));
+    check_launch("x25519_base");
+  });
+  m.def("set_gemm_fold_f64", &set_gemm_fold_f64);
   m.def("colsum", [](int G, int R, int L, uint32_t mod, int value_bytes, uintptr_t vals,
                      uintptr_t out, uintptr_t stream) {
     launch_colsum(G, R, L, mod, value_bytes, P<const void>(vals), P<uint32_t>(out), S(stream));

@@ -390,6 +390,27 @@ int main() {
     bytes(db, dw, 8);
     CHECK(std::memcmp(ho, db, 32) == 0, "x25519 it=%d", it);
   }
+  // 1c. fixed-base X25519 (edwards25519 table) vs the host's scalarmult_base
+  {
+    static const uint32_t table[32 * 8 * kEdEntryWords] = {
+#include "ed25519_base.inc"
+    };
+    for (int it = 0; it < 256; ++it) {
+      uint8_t sc[32], ho[32];
+      hc::os_random(sc, 32);
+      if (it == 0) std::memset(sc, 0, 32);
+      if (it == 1) std::memset(sc, 0xff, 32);
+      if (it == 2) { std::memset(sc, 0x88, 32); }  // every digit at the carry border
+      if (it == 3) { std::memset(sc, 0x77, 32); }
+      hc::x25519_base(ho, sc);
+      uint32_t sw[8], dw[8];
+      words(sw, sc, 8);
+      x25519_base(dw, sw, table);
+      uint8_t db[32];
+      bytes(db, dw, 8);
+      CHECK(std::memcmp(ho, db, 32) == 0, "x25519_base it=%d", it);
+    }
+  }
   // 2. message key derivation vs host crypto_box_seal
   uint8_t pk[32], sk[32], esk[32], epk[32];
   hc::box_keypair(pk, sk);

@@ -91,6 +91,12 @@ void set_key_prio(int open_prio, int powers_prio);
 // grid launched right after it.
 void launch_gate_wait(const uint32_t* gate, uint32_t val, uint32_t timeout_us, hipStream_t s);
 // Standalone batched X25519 (tests / key generation): out[i] = X25519(sc[i], u[i]).
+// X25519(scalar, 9) through the edwards25519 fixed-base table (test hook).
+void launch_x25519_base(int N, const uint32_t* scalars, uint32_t* out, hipStream_t s);
+// launch_seal_setup's kernel: -1 by message count (default), 0 two lanes per message
+// (both ladders side by side: lowest latency), 1 one lane per message with the
+// fixed-base table for the public key (least work)
+void set_seal_many(int mode);
 void launch_x25519(int N, const uint32_t* scalars, const uint32_t* points, uint32_t* out,
                    hipStream_t s);
 
@@ -241,8 +247,9 @@ void launch_sub_mod(int D, uint32_t m, const uint32_t* a, const uint32_t* b, uin
 void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p, const int8_t* A,
                        const int8_t* B, int64_t b_plane, int value_bytes, void* C, int64_t ldc_z,
                        int64_t ldc_m, int64_t ldc_n, int64_t limit, uint32_t* cnt, hipStream_t s);
-// epilogue reductions on the 24-bit multipliers where the modulus allows (default on)
-void set_gemm_fold24(int on);
+// epilogue fold through the double-precision unit: 0 never (integer only), 1 for
+// three-limb fields (default), 2 for four-limb fields too
+void set_gemm_fold_f64(int mode);
 // X limbs [3][P][B][Kp] of packed-Shamir inputs: secrets (canonical) then t draws.
 void launch_pss_x_limbs(int P, int D, int B, int k, int t, int Kp, int limbs, uint32_t p,
                         const int32_t* secrets, RngKeyArg rng, uint64_t owner_base, int8_t* X,

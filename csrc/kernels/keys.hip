@@ -59,6 +59,11 @@ SDA_DEV void derive_msg_key(MsgKey& out, const uint32_t (&shared)[8], const uint
   out.pad[0] = out.pad[1] = 0;
 }
 
+// (j + 1) 256^i B of edwards25519 as y+x, y-x, 2dxy (x25519_base's table, 32 KB)
+__device__ const uint32_t g_ed_base[32 * 8 * kEdEntryWords] = {
+#include "ed25519_base.inc"
+};
+
 // Setup kernels run beside full-chip grids: 4 ladder waves per workgroup pack
 // them onto a quarter as many CUs (a ~150-VGPR ladder wave costs its CU one of
 // the neighbouring grid's workgroups; measured on the round timeline).
@@ -118,6 +123,58 @@ __global__ void __launch_bounds__(kSetupBlock) k_seal_setup(int M, RngKeyArg rng
   for (int i = 0; i < 8; ++i) hdr[i] = epk[i];
 }
 
+// The many-message form (hundreds of thousands of boxes: the many-clerk committees):
+// the launch runs for many rounds of resident waves, so what counts is the work per
+// message, not one ladder's latency. One lane per message; its ephemeral public key
+// comes from the fixed-base table (a fifth of a ladder's multiplications), only the
+// shared point needs the ladder.
+__global__ void __launch_bounds__(kSetupBlock) k_seal_setup_many(int M, RngKeyArg rng, uint64_t owner_base,
+                                                        const uint32_t* __restrict__ key_idx,
+                                                        const uint32_t* __restrict__ pks, uint8_t* ct,
+                                                        uint64_t stride, MsgKey* keys, uint32_t* err,
+                                                        uint32_t* gate, uint32_t gate_val) {
+  signal_dispatched(gate, gate_val);
+  __builtin_amdgcn_s_setprio(3);  // see k_seal_setup
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= M) return;
+  RngKey rk;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rk.k[i] = rng.k[i];
+  uint32_t w[16];
+  rng_block(w, rk, stream_id(kPurposeEphemeral, owner_base + (uint64_t)j), 0);
+  uint32_t esk[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) esk[i] = w[i];
+  uint32_t pk[8];
+  const uint32_t* pkp = pks + 8 * (size_t)key_idx[j];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pk[i] = pkp[i];
+  uint32_t epk[8], shared[8];
+  x25519_base(epk, esk, g_ed_base);
+  x25519(shared, esk, pk);
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc |= shared[i];
+  if (acc == 0) atomicOr(err, kErrBadKey);
+  MsgKey mk;
+  derive_msg_key(mk, shared, epk, pk);
+  keys[j] = mk;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(ct + (size_t)j * stride);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) hdr[i] = epk[i];
+}
+
+__global__ void __launch_bounds__(64) k_x25519_base(int N, const uint32_t* __restrict__ sc, uint32_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  uint32_t a[8], o[8];
+#pragma unroll
+  for (int w = 0; w < 8; ++w) a[w] = sc[8 * (size_t)i + w];
+  x25519_base(o, a, g_ed_base);
+#pragma unroll
+  for (int w = 0; w < 8; ++w) out[8 * (size_t)i + w] = o[w];
+}
+
 __global__ void __launch_bounds__(kSetupBlock) k_open_setup(int M, const uint32_t* __restrict__ key_idx,
                                                    const uint32_t* __restrict__ sks,
                                                    const uint32_t* __restrict__ pks,
@@ -162,6 +219,8 @@ __global__ void __launch_bounds__(64) k_x25519(int N, const uint32_t* __restrict
 
 }  // namespace
 
+static int g_seal_many = -1;  // -1: by message count; 0 / 1: force the pair / many-message form
+void set_seal_many(int mode) { g_seal_many = mode; }
 static int g_open_prio = 0;
 int g_powers_prio = 0;
 void set_key_prio(int open_prio, int powers_prio) {
@@ -173,6 +232,15 @@ void launch_seal_setup(int M, RngKeyArg rng, uint64_t owner_base, const uint32_t
                        const uint32_t* pks, uint8_t* ct, uint64_t stride, MsgKey* keys,
                        uint32_t* err, uint32_t* gate, uint32_t gate_val, hipStream_t s) {
   if (M <= 0) return;
+  // a launch of several rounds of resident waves (~200k lanes at three ladder waves
+  // per SIMD) is bound by its work, not by a ladder's latency
+  const bool many = g_seal_many < 0 ? M >= 65536 : g_seal_many != 0;
+  if (many) {
+    hipLaunchKernelGGL(k_seal_setup_many, dim3((unsigned)((M + kSetupBlock - 1) / kSetupBlock)),
+                       dim3(kSetupBlock), 0, s, M, rng, owner_base, key_idx, pks, ct, stride, keys,
+                       err, gate, gate_val);
+    return;
+  }
   const int64_t threads = 2 * (int64_t)M;
   hipLaunchKernelGGL(k_seal_setup, dim3((unsigned)((threads + kSetupBlock - 1) / kSetupBlock)),
                      dim3(kSetupBlock), 0, s, M, rng,
@@ -191,6 +259,11 @@ void launch_open_setup(int M, const uint32_t* key_idx, const uint32_t* sks, cons
 void launch_gate_wait(const uint32_t* gate, uint32_t val, uint32_t timeout_us, hipStream_t s) {
   hipLaunchKernelGGL(k_gate_wait, dim3(1), dim3(64), 0, s, gate, val,
                      (uint64_t)timeout_us * 100);
+}
+
+void launch_x25519_base(int N, const uint32_t* scalars, uint32_t* out, hipStream_t s) {
+  if (N <= 0) return;
+  hipLaunchKernelGGL(k_x25519_base, dim3((N + 63) / 64), dim3(64), 0, s, N, scalars, out);
 }
 
 void launch_x25519(int N, const uint32_t* scalars, const uint32_t* points, uint32_t* out,

@@ -58,27 +58,25 @@ SDA_DEV uint32_t mod24(uint32_t w, const Mod24& P) {
   const uint32_t q = (uint32_t)(((uint64_t)((w << P.k) & 0xffffffu) * (uint64_t)(P.c & 0xffffffu)) >> 32);
   return w - (q & 0xffffffu) * (P.m & 0xffffffu);  // q, m < 2^24: a 24-bit multiply-subtract
 }
-// Exact reduction of any 32-bit w by a modulus 2^16 <= m < 2^24 on the full-rate
-// 24-bit multipliers: with 2^(L-1) <= m < 2^L and mu = floor(2^(23+L) / m) < 2^24,
-//   q = (((w >> 8) * mu) >> 32) >> (L - 17)  is floor(w / m) or one less
-// (dropping w's low byte costs < 256/m, mu's rounding < 2^(9-L)), so one conditional
-// subtraction finishes. Seven issue slots against eleven for mod32.
-struct Mod24w {
-  uint32_t mu, sh, m;  // mu == 0: not available for this modulus
+// Exact reduction of an integer 0 <= v < 2^53 through the double-precision unit (full
+// rate on this chip, like the 32-bit integer multiplies): q = trunc(v * (1/m)) is
+// floor(v / m) or off by one (v / m < 2^33 and the two roundings move it by less than
+// 2^-18), v - q m is then exact in one fused multiply-add, and two corrections bring
+// it into [0, m). Eleven instructions, whatever v's size -- a 64-bit Barrett step
+// (mod64) takes about thirty.
+struct ModF64 {
+  double m, inv;
 };
-inline Mod24w make_mod24w(uint32_t m) {
-  if (m < (1u << 16) || m >= (1u << 24)) return Mod24w{0, 0, m};
-  uint32_t L = 17;
-  while ((m >> L) != 0) ++L;  // 2^(L-1) <= m < 2^L
-  const uint64_t mu = (1ull << (23 + L)) / m;
-  if (mu >= (1u << 24)) return Mod24w{0, 0, m};  // m a power of two
-  return Mod24w{(uint32_t)mu, L - 17, m};
-}
-SDA_DEV uint32_t mod24w(uint32_t w, const Mod24w& P) {
-  const uint32_t t = (uint32_t)(((uint64_t)((w >> 8) & 0xffffffu) * (uint64_t)(P.mu & 0xffffffu)) >> 32);
-  const uint32_t q = t >> P.sh;
-  const uint32_t r = w - (q & 0xffffffu) * (P.m & 0xffffffu);  // in [0, 2 m)
-  return min(r, r - P.m);  // r - m wraps to a huge value when r < m
+inline ModF64 make_modf64(uint32_t m) { return ModF64{(double)m, m ? 1.0 / (double)m : 0.0}; }
+SDA_DEV uint32_t modf64(uint64_t v, const ModF64& P) {
+  const double vd = (double)(int64_t)v;
+  const double q = __builtin_trunc(vd * P.inv);
+  int32_t r = (int32_t)__builtin_fma(-q, P.m, vd);  // in (-m, 2m)
+  const int32_t m = (int32_t)P.m;
+  r += (r >> 31) & m;
+  r -= m;
+  r += (r >> 31) & m;
+  return (uint32_t)r;
 }
 SDA_DEV uint32_t mod64(uint64_t v, const ModParams& P) {
   uint64_t q = __umul64hi(v, P.mu64);

@@ -8,7 +8,7 @@
 // non-negative), so every limb product fits the i8 MFMA and a K-sum of up to L
 // limb products per degree stays below 2^31 (K * 127^2 * L < 2^31). The L^2
 // limb products per K-step go into 2L - 1 accumulators by degree d = i + j;
-// the epilogue folds sum_d (acc_d mod p) * (2^(7d) mod p) with Barrett steps.
+// the epilogue folds sum_d acc_d 2^(7d) mod p (kFold below).
 //
 // Layouts: A limbs [L][M][Kp] (row-major, k contiguous), B limbs
 // [L][batch][N][Kp] (B stored transposed: each column contiguous in k); Kp is a
@@ -25,16 +25,21 @@
 // are stored XOR-swizzled (chunk ^ {0,2,3,1}[(row >> 2) & 3]) so that the 16
 // lanes ds_read_b128 services together (which mix two chunk indices and three
 // row ranges) hit 16 different 16-byte slots of the 256-byte bank row.
-// K = t + k is short (255 -> 4 steps), so the epilogue matters as much as the
-// MFMAs: with p < 2^21 the 2L - 1 degree sums fold by a 32-bit Horner chain
-// (s <- (s * 2^7 + acc_d) mod p, every intermediate below 2^32) instead of
-// 64-bit multiply-adds.
+// K = t + k is short (255 -> 4 steps), so the epilogue matters more than the MFMAs
+// (728 clerks x 1000 participants: 288 MFMAs and ~2,200 VALU instructions per wave;
+// the kernel's 26 ms are those two issue streams back to back, 7 + 14 ms). What
+// was tried on it and measured neutral: reductions on the 24-bit multipliers (every
+// 32-bit integer multiply is full rate on this chip), operand reuse through the
+// L2 (the block id remap below), the fold through the double-precision unit (-1 ms
+// with three limbs).
 //
 // Share generation also needs every sealed box's varint length per 4096-value
 // tile before the encoder can place its bytes (kernels.hpp, launch_count). With
 // `cnt` the epilogue adds them up itself -- the lengths of a lane's outputs per
 // row, summed over the 16 lanes of a row group on the VALU (DPP), one atomic add
 // per (row, wave) -- instead of a second pass over the stored shares.
+#include <algorithm>
+
 #include "block_utils.hpp"
 #include "device_crypto.hpp"
 #include "kernels.hpp"
@@ -52,15 +57,32 @@ SDA_DEV int swz(int row, int chunk) {  // position of a row's 16-byte chunk insi
   return chunk ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3);  // {0, 2, 3, 1}
 }
 
-// kFold: how the epilogue folds the degree sums. 0: Horner chain with mod32 (p <
-// 2^24: s < p and acc_d < 2^31 keep s * 2^7 + acc_d below 2^32); 1: the same chain on
-// the 24-bit multipliers (mod24w, 2^16 <= p < 2^24: both of the reference's large
-// fields); 2: 64-bit multiply-adds by 2^(7d) mod p and one 64-bit reduction (p >= 2^24).
+// kFold: how the epilogue folds the degree sums acc_d (< 2^31) into sum_d acc_d 2^(7d)
+// mod p. 1: in 64-bit integers -- one multiply-add per degree -- reduced through the
+// double-precision unit (modf64): all five degrees at once with three limbs (the
+// caller checks sum < 2^53), degrees 3..6 first and then the rest with four. 0: a
+// Horner chain of 32-bit Barrett steps (p < 2^24: s < p and acc_d < 2^31 keep
+// s * 2^7 + acc_d below 2^32). 2: 64-bit multiply-adds by 2^(7d) mod p and one 64-bit
+// Barrett reduction (any p < 2^28). 0 and 2 are the integer-only references.
+// Block id -> tile. K is short, so the kernel lives on operand reuse between blocks: a
+// column panel of B (128 columns of one batch) is read by every row block, a row block
+// of A by every panel. Consecutive block ids go round the 8 XCDs, each with its own
+// L2: ids congruent mod 8 share one. Each such class walks super-tiles of gm row
+// blocks x gp panels (row blocks fastest), sized so that a super-tile's operands stay
+// in the 4 MB L2: every operand tile is then fetched from HBM / the Infinity Cache once
+// per super-tile instead of once per block (728 clerks: the 7.7 GB of B limbs went
+// through 12 times). Ragged edges are blocks that exit at once.
+struct GemmGrid {
+  int gx, gy, panels;  // column blocks per batch, row blocks, gx * batches
+  int gm, gp, tiles_m;
+};
+constexpr int kXcds = 8;
+
 template <typename VT, int kLimbs, int kFold>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
-    k_modgemm_i8(int M, int N, int Kp, ModParams mp, Mod24w m24, const int8_t* __restrict__ A,
-                 const int8_t* __restrict__ B, int64_t b_batch, VT* __restrict__ C,
-                 int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit,
+    k_modgemm_i8(int M, int N, int Kp, int batches, GemmGrid gg, ModParams mp, ModF64 mf,
+                 const int8_t* __restrict__ A, const int8_t* __restrict__ B, int64_t b_batch,
+                 VT* __restrict__ C, int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit,
                  uint32_t* __restrict__ cnt, int cnt_tiles) {
   constexpr int kRows = kBM + kBN;                       // staged rows per limb
   constexpr int kStage = kLimbs * kRows * kBK;           // bytes per buffer
@@ -68,8 +90,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   __shared__ __attribute__((aligned(16))) int8_t lds[2 * kStage];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m_blk = blockIdx.y * kBM, n_blk = blockIdx.x * kBN;
-  const int z = blockIdx.z;
+  int m_blk, n_blk, z;
+  {
+    const int cls = blockIdx.x % kXcds, seq = blockIdx.x / kXcds;
+    const int per = gg.gm * gg.gp;
+    const int tile = seq / per, i = seq % per;
+    const int mb = (tile % gg.tiles_m) * gg.gm + i % gg.gm;
+    const int panel = ((tile / gg.tiles_m) * gg.gp + i / gg.gm) * kXcds + cls;
+    if (mb >= gg.gy || panel >= gg.panels) return;  // block-uniform
+    m_blk = mb * kBM;
+    n_blk = (panel % gg.gx) * kBN;
+    z = panel / gg.gx;
+  }
   const int64_t a_plane = (int64_t)M * Kp;
   const int8_t* Bz = B + (int64_t)z * (int64_t)N * Kp;
 
@@ -158,10 +190,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
     for (int d = 0; d < kDeg; ++d) w[d] = (uint32_t)(((uint64_t)1 << (kLimbBits * d)) % mp.m);
   }
-  auto red = [&](uint32_t x) -> uint32_t {
-    if constexpr (kFold == 1) return mod24w(x, m24);
-    else return mod32(x, mp);
-  };
   const int row0 = m_blk + wm * 32 + 4 * (lane >> 4);
   const int col0 = n_blk + wn * 64 + (lane & 15);
   const int64_t base = (int64_t)z * ldc_z + (int64_t)row0 * ldc_m + (int64_t)col0 * ldc_n;
@@ -178,11 +206,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int j = 0; j < 4; ++j, idx += step_j) {
         if (col0 + 16 * j >= N) continue;
         uint32_t out;
-        if constexpr (kFold != 2) {
-          // acc_d < 2^31, s < p < 2^24: s * 2^7 + acc_d < 2^32
-          uint32_t s = red((uint32_t)acc[i][j][kDeg - 1][r]);
+        if constexpr (kFold == 1) {
+          constexpr int kSplit = kLimbs == 3 ? 0 : 3;  // degrees >= kSplit are folded first
+          uint64_t hi = 0;
+          if constexpr (kSplit > 0) {
 #pragma unroll
-          for (int d = kDeg - 2; d >= 0; --d) s = red((s << kLimbBits) + (uint32_t)acc[i][j][d][r]);
+            for (int d = kDeg - 1; d >= kSplit; --d)
+              hi += (uint64_t)(uint32_t)acc[i][j][d][r] << (kLimbBits * (d - kSplit));
+            hi = (uint64_t)modf64(hi, mf) << (kLimbBits * kSplit);
+          }
+#pragma unroll
+          for (int d = (kSplit > 0 ? kSplit : kDeg) - 1; d >= 0; --d)
+            hi += (uint64_t)(uint32_t)acc[i][j][d][r] << (kLimbBits * d);
+          out = modf64(hi, mf);
+        } else if constexpr (kFold == 0) {
+          // acc_d < 2^31, s < p < 2^24: s * 2^7 + acc_d < 2^32
+          uint32_t s = mod32((uint32_t)acc[i][j][kDeg - 1][r], mp);
+#pragma unroll
+          for (int d = kDeg - 2; d >= 0; --d) s = mod32((s << kLimbBits) + (uint32_t)acc[i][j][d][r], mp);
           out = s;
         } else {
           uint64_t s = 0;
@@ -216,7 +257,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         const int row = row0 + 16 * i + 2 * h + q;
         const uint32_t v = (sum >> (16 * q)) & 0xffffu;
         if (row < M && v != 0)
-          atomicAdd(&cnt[((int64_t)row * gridDim.z + z) * cnt_tiles + tile], v);
+          atomicAdd(&cnt[((int64_t)row * batches + z) * cnt_tiles + tile], v);
       }
     }
 }
@@ -301,20 +342,43 @@ __global__ void __launch_bounds__(256)
 
 }  // namespace
 
-static int g_gemm_fold24 = 1;
-void set_gemm_fold24(int on) { g_gemm_fold24 = on; }
+static int g_gemm_fold_f64 = 1;  // 0 never, 1 three-limb fields (default), 2 four-limb ones too
+void set_gemm_fold_f64(int mode) { g_gemm_fold_f64 = mode; }
 
 void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p, const int8_t* A,
                        const int8_t* B, int64_t b_plane, int value_bytes, void* C, int64_t ldc_z,
                        int64_t ldc_m, int64_t ldc_n, int64_t limit, uint32_t* cnt, hipStream_t s) {
   if (M <= 0 || N <= 0 || batches <= 0) return;
   ModParams mp = make_mod_params(p);
-  const Mod24w m24 = make_mod24w(p);
-  const int fold = p >= (1u << 24) ? 2 : (m24.mu != 0 && g_gemm_fold24 ? 1 : 0);
-  dim3 grid((N + kBN - 1) / kBN, (M + kBM - 1) / kBM, batches);
+  const ModF64 mf = make_modf64(p);
+  // three limbs fold all five degrees in one 64-bit sum: acc_d <= Kp 127^2 min(d + 1, 5 - d)
+  const bool fits53 = limbs == 4 || (uint64_t)Kp * 127 * 127 * ((1ull << 28) + (2ull << 21) + (3ull << 14) +
+                                                               (2ull << 7) + 1) < (1ull << 53);
+  // measured on the share GEMMs of the two large reference fields: three limbs 29.6 ->
+  // 28.5 ms with the double-precision fold, four limbs 25.6 -> 27.6 ms (its two-stage
+  // fold spills next to 224 accumulator registers): default for three limbs only
+  const bool f64 = g_gemm_fold_f64 == 2 || (g_gemm_fold_f64 == 1 && limbs == 3);
+  const int fold = f64 && fits53 ? 1 : (p >= (1u << 24) ? 2 : 0);
+  GemmGrid gg;
+  gg.gx = (N + kBN - 1) / kBN;
+  gg.gy = (M + kBM - 1) / kBM;
+  gg.panels = gg.gx * batches;
+  {
+    // super-tile: all row blocks if they are few, else 8; panels to fill ~2 MB of L2
+    const int64_t a_tile = (int64_t)kBM * Kp * limbs, b_panel = (int64_t)kBN * Kp * limbs;
+    gg.gm = gg.gy <= 16 ? gg.gy : 8;
+    const int64_t room = (2 << 20) - gg.gm * a_tile;
+    gg.gp = (int)std::max<int64_t>(1, std::min<int64_t>(8, room / b_panel));
+    gg.tiles_m = (gg.gy + gg.gm - 1) / gg.gm;
+  }
+  const int panels_x = (gg.panels + kXcds - 1) / kXcds;          // panels per id class
+  const int tiles_p = (panels_x + gg.gp - 1) / gg.gp;
+  const int64_t blocks = (int64_t)kXcds * gg.tiles_m * tiles_p * gg.gm * gg.gp;
+  if (blocks > 0x7fffffff) return;  // cannot happen below 2^31 output tiles
+  dim3 grid((unsigned)blocks);
   const int cnt_tiles = (N + kTileValues - 1) / kTileValues;
 #define SDA_GEMM(VT, L, F)                                                                        \
-  hipLaunchKernelGGL((k_modgemm_i8<VT, L, F>), grid, dim3(256), 0, s, M, N, Kp, mp, m24, A, B, b_plane, \
+  hipLaunchKernelGGL((k_modgemm_i8<VT, L, F>), grid, dim3(256), 0, s, M, N, Kp, batches, gg, mp, mf, A, B, b_plane, \
                      (VT*)C, ldc_z, ldc_m, ldc_n, limit, cnt, cnt_tiles)
 #define SDA_GEMM_VT(VT)                                                     \
   do {                                                                      \

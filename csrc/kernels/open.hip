@@ -245,8 +245,8 @@ SDA_DEV uint32_t spread4(uint32_t bits4) {  // 4 bits -> 0xff per set bit, byte 
 // continuation bytes at its end to the next lane, which adds them from the four
 // bytes before its own; five-byte varints raise `redo`.
 //
-// kSwz: the accumulator with one pad word after every 32 (rank x at word
-// x + (x >> 5)). A lane's 64 bytes hold 64 / (code length) elements, so with codes
+// kSwz: the accumulator with one pad word after every 32 (or 16) ranks (rank x at
+// word x + (x >> 5)). A lane's 64 bytes hold 64 / (code length) elements, so with codes
 // that are (nearly) all two, three or four bytes long the lanes' ranks are 32,
 // 21.33 or 16 words apart and the same ds_add of every lane falls into one, three
 // or two banks; in 33-word rows those strides step through all of them. Costs two
@@ -262,12 +262,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMa
   // three (kMaxBytes = 4 only): the field's codes have at most three bytes, a fourth
   // raises `redo` (the caller sized the participant groups for 21-bit codes)
   constexpr int kWaveBytes = 64 * 64;
-  constexpr int kAccWords = kSwz ? kSumAcc + kSumAcc / 32 + 1 : kSumAcc;
+  // pad stride: every 32 words for two-byte codes (ranks 32 apart -> 33), every 16 for
+  // the long ones (21.33 / 16 apart -> 22.67 / 17: odd and even banks alike)
+  constexpr int kPadShift = kMaxBytes > 2 ? 4 : 5;
+  constexpr int kAccWords = kSwz ? kSumAcc + (kSumAcc >> kPadShift) + 1 : kSumAcc;
   __shared__ uint32_t acc[kAccWords];
   __shared__ uint32_t info[kBlock][4];
   // acc[byte offset / 4] += v, through the padded layout when kSwz
   auto add = [&](uint32_t byte_off, uint32_t v) {
-    lds_add(acc, kSwz ? byte_off + ((byte_off >> 7) << 2) : byte_off, v);
+    lds_add(acc, kSwz ? byte_off + ((byte_off >> (kPadShift + 2)) << 2) : byte_off, v);
   };
   const int t = blockIdx.x, r = blockIdx.y, g = blockIdx.z, R = gridDim.y;
   const int T = gridDim.x;
@@ -471,7 +474,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMa
   uint32_t* out = part + ((size_t)g * R + r) * L + E0;
   for (uint32_t i = tid; i < W; i += kBlock) {
     const uint32_t x = kSumMargin + i;
-    out[i] = acc[kSwz ? x + (x >> 5) : x];
+    out[i] = acc[kSwz ? x + (x >> kPadShift) : x];
   }
   if (bad) atomicOr(redo, 1u);
   if (malformed) atomicOr(err, kErrMalformed);
@@ -629,8 +632,12 @@ void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* p
   // generic one then runs only if `redo` was raised (it rewrites every slab)
   // (codes of 2 bytes below 2^14, of 4 bytes below 2^28: moduli up to 2^13 / 2^27)
   const bool lean = g_decode_lean && redo != nullptr && m <= (1u << 27);
-  // padded accumulator rows where the codes are (nearly) all of one length
-  const bool swz = g_decode_swz < 0 ? m > 2048u : g_decode_swz != 0;
+  // padded accumulator rows where they measured faster: fields of (nearly) all
+  // two-byte codes (ranks 32 words apart) and of three-byte codes (21.33 apart: 728
+  // clerks x 1000 participants, 24.9 -> 22.9 ms); with mostly four-byte codes the two
+  // extra instructions per add cost more than the conflicts (5.8 -> 6.7 ms)
+  const bool three = 2ull * (m - 1) < (1ull << 21);
+  const bool swz = g_decode_swz < 0 ? (m > 2048u && (m <= 8192u || three)) : g_decode_swz != 0;
   if (lean && m <= 8192u) {
     auto kern = swz ? k_decode_sum_z<2, true> : k_decode_sum_z<2, false>;
     hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S, pre,
@@ -638,7 +645,7 @@ void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* p
   } else if (lean) {  // canonical codes 2 (m - 1) below 2^21 have at most three bytes
     auto kern = swz ? k_decode_sum_z<4, true> : k_decode_sum_z<4, false>;
     hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S, pre,
-                       tile_sub, part, redo, err, 2ull * (m - 1) < (1ull << 21) ? 1 : 0);
+                       tile_sub, part, redo, err, three ? 1 : 0);
   }
   const uint32_t* gate = lean ? redo : nullptr;
   if (m < 65536u)

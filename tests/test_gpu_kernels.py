@@ -36,6 +36,53 @@ def _keytable(native, cuda, count):
     return KeyTable.generate(count, cuda)
 
 
+def test_x25519_fixed_base_matches_ladder(cuda, native):
+    """The edwards25519 fixed-base route to an ephemeral public key (64 table
+    additions) against the ladder on u = 9 and against the host."""
+    from sda_amd._native import gpu
+    n = 300
+    sc = torch.randint(-2 ** 31, 2 ** 31 - 1, (n, 8), dtype=torch.int32)
+    sc[0] = 0
+    sc[1] = -1
+    sc[2] = 0x77777777
+    sc[3] = 0x88888888 - (1 << 32)  # every digit at the carry border
+    nine = torch.zeros(n, 8, dtype=torch.int32)
+    nine[:, 0] = 9
+    d_sc, d_pt = sc.to(cuda), nine.to(cuda)
+    a = torch.empty(n, 8, dtype=torch.int32, device=cuda)
+    b = torch.empty(n, 8, dtype=torch.int32, device=cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    gpu().x25519(n, d_sc.data_ptr(), d_pt.data_ptr(), a.data_ptr(), st)
+    gpu().x25519_base(n, d_sc.data_ptr(), b.data_ptr(), st)
+    assert torch.equal(a, b)
+    for j in (0, 1, 5):
+        host = native.crypto.x25519_base(sc[j].numpy().tobytes())
+        assert b[j].cpu().numpy().tobytes() == host
+
+
+@pytest.mark.parametrize("many", [0, 1])
+def test_seal_setup_forms_open_on_host(cuda, native, many):
+    """Both key-agreement kernels of the seal side -- two lanes per message with two
+    ladders, one lane with the fixed-base table -- give boxes the host opens."""
+    from sda_amd._native import gpu
+    from sda_amd.ops.sealed import seal
+    keys = _keytable(native, cuda, 2)
+    M, L, m = 70, 300, 433
+    vals64 = torch.randint(0, m, (M, L), dtype=torch.int64)
+    kidx = torch.tensor([j % 2 for j in range(M)], dtype=torch.int32, device=cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    gpu().set_seal_many(many)
+    try:
+        arena = seal(vals64.to(torch.int16).to(cuda), kidx, keys.pks, os.urandom(32), 0, err, m)
+        blobs = arena.to_blobs()
+    finally:
+        gpu().set_seal_many(-1)
+    assert int(err.item()) == 0
+    for j in range(M):
+        pt = native.crypto.box_seal_open(blobs[j], keys.pk_bytes[j % 2], keys.sk_bytes[j % 2])
+        assert pt is not None and varint_decode(pt) == vals64[j].tolist(), j
+
+
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("L,modulus", [(1, 433), (10, 433), (5000, 433), (20000, 433),
                                        (3000, 2 ** 31 - 1), (70000, 65521), (150001, 433),

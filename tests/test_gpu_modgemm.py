@@ -10,14 +10,16 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("prime,fold24", [(746497, 1), (746497, 0), (5038849, 1), (5038849, 0),
-                                          (433, 1), (16777213, 1), ((1 << 27) - 39, 1)])
+@pytest.mark.parametrize("prime,fold24", [(746497, 1), (746497, 0), (5038849, 2), (5038849, 0),
+                                          (433, 1), (433, 0), (16777213, 2), (16777213, 1),
+                                          ((1 << 27) - 39, 2), ((1 << 27) - 39, 0),
+                                          ((1 << 28) - 57, 2)])
 @pytest.mark.parametrize("M,N,K,Z", [(37, 45, 100, 2), (64, 64, 64, 1), (5, 300, 255, 3),
                                      (130, 17, 700, 1)])
 def test_modgemm_matches_torch(cuda, prime, fold24, M, N, K, Z):
-    """Every epilogue: the Horner fold on the 24-bit multipliers (2^16 <= p < 2^24),
-    the same with 32-bit Barrett steps (forced, and for small p), and the 64-bit fold
-    (p >= 2^24)."""
+    """Every epilogue: the 64-bit fold reduced through the double-precision unit (the
+    default), and with it switched off the Horner chain of 32-bit Barrett steps
+    (p < 2^24) and the 64-bit Barrett fold (p >= 2^24)."""
     from sda_amd._native import gpu
     from sda_amd.ops import gpu as G
 
@@ -29,12 +31,12 @@ def test_modgemm_matches_torch(cuda, prime, fold24, M, N, K, Z):
     Al = G.limbs_of(A.to(torch.int32).cuda(), Kp, L)
     Bl = torch.stack([G.limbs_of(Bm[z].to(torch.int32).cuda(), Kp, L) for z in range(Z)], 1)
     out = torch.zeros(Z * M * N, dtype=torch.int32, device="cuda")
-    gpu().set_gemm_fold24(fold24)
+    gpu().set_gemm_fold_f64(fold24)
     try:
         G.modgemm_i8(Al.contiguous(), Bl.contiguous(), prime, out, ldc_z=M * N, ldc_m=N, ldc_n=1,
                      limit=Z * M * N)
     finally:
-        gpu().set_gemm_fold24(1)
+        gpu().set_gemm_fold_f64(1)
     # exact reference: split K to keep int64 products exact
     ref = torch.stack([(A @ Bm[z].T) % prime for z in range(Z)]) if prime < 2 ** 21 else \
         torch.stack([sum((A[:, i:i + 1] * Bm[z][:, i:i + 1].T) % prime for i in range(K)) % prime
