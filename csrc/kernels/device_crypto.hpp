@@ -690,8 +690,8 @@ SDA_DEV void fe10_to_words(uint32_t (&w)[8], const Fe10& a) {
   }
 }
 
-// X25519(scalar, u): RFC 7748 ladder. Words are little-endian.
-SDA_DEV void x25519(uint32_t (&out)[8], const uint32_t (&scalar)[8], const uint32_t (&u)[8]) {
+// RFC 7748 ladder: X25519(scalar, u) = x2 / z2 (0 when z2 = 0). Words are little-endian.
+SDA_DEV void x25519_xz(Fe10& x2_out, Fe10& z2_out, const uint32_t (&scalar)[8], const uint32_t (&u)[8]) {
   uint32_t k[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) k[i] = scalar[i];
@@ -720,6 +720,12 @@ SDA_DEV void x25519(uint32_t (&out)[8], const uint32_t (&scalar)[8], const uint3
   }
   fe10_cswap(x2, x3, swap);
   fe10_cswap(z2, z3, swap);
+  x2_out = x2;
+  z2_out = z2;
+}
+SDA_DEV void x25519(uint32_t (&out)[8], const uint32_t (&scalar)[8], const uint32_t (&u)[8]) {
+  Fe10 x2, z2;
+  x25519_xz(x2, z2, scalar, u);
   fe10_to_words(out, fe10_mul(x2, fe10_invert(z2)));
 }
 
@@ -782,7 +788,8 @@ SDA_DEV GeP1 ge_dbl(const Fe10& X, const Fe10& Y, const Fe10& Z) {
   r.T = fe10_sub(b, r.Z);
   return r;
 }
-SDA_DEV void x25519_base(uint32_t (&out)[8], const uint32_t (&scalar)[8], const uint32_t* table) {
+// X25519(scalar, 9) = num / den
+SDA_DEV void x25519_base_nd(Fe10& num_out, Fe10& den_out, const uint32_t (&scalar)[8], const uint32_t* table) {
   uint32_t k[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) k[i] = scalar[i];
@@ -834,9 +841,26 @@ SDA_DEV void x25519_base(uint32_t (&out)[8], const uint32_t (&scalar)[8], const 
   h = ge_p1_to_p3(r);
 #pragma unroll 1
   for (int i = 0; i < 64; i += 2) step(i);
-  const Fe10 num = fe10_add_nc(h.Z, h.Y);
-  const Fe10 den = fe10_sub(h.Z, h.Y);
+  num_out = fe10_add(h.Z, h.Y);
+  den_out = fe10_sub(h.Z, h.Y);
+}
+SDA_DEV void x25519_base(uint32_t (&out)[8], const uint32_t (&scalar)[8], const uint32_t* table) {
+  Fe10 num, den;
+  x25519_base_nd(num, den, scalar, table);
   fe10_to_words(out, fe10_mul(num, fe10_invert(den)));
+}
+// Both halves of a sealed box's key agreement, epk = esk . 9 and shared = esk . pk,
+// with one field inversion for the two (1 / (z2 den), then times the other
+// denominator). A zero z2 (a low-order pk: the shared point is rejected anyway) makes
+// both outputs zero.
+SDA_DEV void x25519_seal_pair(uint32_t (&epk)[8], uint32_t (&shared)[8], const uint32_t (&esk)[8],
+                              const uint32_t (&pk)[8], const uint32_t* table) {
+  Fe10 num, den, x2, z2;
+  x25519_base_nd(num, den, esk, table);
+  x25519_xz(x2, z2, esk, pk);
+  const Fe10 inv = fe10_invert(fe10_mul(z2, den));
+  fe10_to_words(epk, fe10_mul(num, fe10_mul(inv, z2)));
+  fe10_to_words(shared, fe10_mul(x2, fe10_mul(inv, den)));
 }
 
 // ------------------------------------------------------------------ varint --

@@ -409,6 +409,18 @@ int main() {
       uint8_t db[32];
       bytes(db, dw, 8);
       CHECK(std::memcmp(ho, db, 32) == 0, "x25519_base it=%d", it);
+      // ... and the pair with a shared inversion against the two separate routes
+      uint8_t pt[32], hs[32];
+      hc::os_random(pt, 32);
+      hc::x25519(hs, sc, pt);
+      uint32_t pw[8], ew[8], shw2[8];
+      words(pw, pt, 8);
+      x25519_seal_pair(ew, shw2, sw, pw, table);
+      uint8_t eb[32], sb[32];
+      bytes(eb, ew, 8);
+      bytes(sb, shw2, 8);
+      CHECK(std::memcmp(ho, eb, 32) == 0, "seal pair epk it=%d", it);
+      CHECK(std::memcmp(hs, sb, 32) == 0, "seal pair shared it=%d", it);
     }
   }
   // 2. message key derivation vs host crypto_box_seal

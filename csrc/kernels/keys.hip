@@ -150,8 +150,7 @@ __global__ void __launch_bounds__(kSetupBlock) k_seal_setup_many(int M, RngKeyAr
 #pragma unroll
   for (int i = 0; i < 8; ++i) pk[i] = pkp[i];
   uint32_t epk[8], shared[8];
-  x25519_base(epk, esk, g_ed_base);
-  x25519(shared, esk, pk);
+  x25519_seal_pair(epk, shared, esk, pk, g_ed_base);
   uint32_t acc = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) acc |= shared[i];

@@ -20,7 +20,6 @@ ChaCha20 streams (one per participant and purpose).
 from __future__ import annotations
 
 import collections
-import os
 from dataclasses import dataclass, field
 from typing import Optional, Sequence
 
@@ -34,13 +33,8 @@ from .ops.sealed import (Arena, KeySet, open_, open_data, open_setup, open_sum, 
 from .utils.trace import tracing_enabled
 
 _TRACE = tracing_enabled()
-# Experimental schedule switch: queue the clerks' key agreement behind the share
-# kernel instead of beside it (A/B measurement of side-stream interference).
-_OPEN_AFTER_SHARE = os.environ.get("SDA_OPEN_AFTER_SHARE", "1") == "1"
-# "open,powers" wave priorities of the side-stream key kernels (experiments)
-_KEY_PRIO = os.environ.get("SDA_KEY_PRIO")
-# unchecked rounds the host may queue ahead of the GPU (measurements of the unbounded case)
-_MAX_INFLIGHT = int(os.environ.get("SDA_MAX_INFLIGHT", "2"))
+# unchecked rounds the host may queue ahead of the GPU (see DeviceAggregator.throttle)
+_MAX_INFLIGHT = 2
 
 
 class AggregationError(RuntimeError):
@@ -150,9 +144,6 @@ class DeviceAggregator:
             self.vdtype = torch.uint8  # a field element per byte
         self.time_stages = time_stages
         self._round = 0
-        if _KEY_PRIO:
-            from ._native import gpu
-            gpu().set_key_prio(*[int(x) for x in _KEY_PRIO.split(",")])
         if isinstance(spec.sharing, PackedShamir):
             p = spec.sharing.native()
             p.validate()
@@ -412,15 +403,13 @@ class DeviceAggregator:
                 ev_openkeys.record(side)
             return ko_clerk, ko_mask, ev_openkeys
 
-        if not _OPEN_AFTER_SHARE:
-            ko_clerk, ko_mask, ev_openkeys = open_keys()
-
         # ---- participants: mask + share, then encrypt (waits for the seal keys)
         G.gate_wait(gate)  # the setup waves are resident before the share grid
         shares, cnt, mask_vals, mask_cnt = self._share(secrets, rng_key, owner_base, err)
-        if _OPEN_AFTER_SHARE:
-            side.wait_stream(main)
-            ko_clerk, ko_mask, ev_openkeys = open_keys()
+        # the clerks' key agreement queues behind the share kernel, not beside it (beside
+        # it, its ladder waves took register space from the share grid: measured slower)
+        side.wait_stream(main)
+        ko_clerk, ko_mask, ev_openkeys = open_keys()
         for t in [ks_clerk, ks_mask, ko_mask] + ko_clerk:
             if t is not None:
                 t.record_stream(main)

@@ -19,7 +19,6 @@ bytes ``[0, 48 + pt_len[j])`` are a wire-format `Encryption` blob.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 
 import torch
@@ -156,8 +155,8 @@ class KeySet:
 # LDS (k_encode_encrypt<.., true>) instead of a separate pass over the stored
 # ciphertext (k_mac_chunks<0>). Saves 5.5 GB of HBM reads per headline round but
 # measured slower (the encode kernel is issue-bound; +1.4 ms against 1.0 ms saved),
-# so it is off unless SDA_FUSED_SEAL_MAC=1.
-FUSED_SEAL_MAC = os.environ.get("SDA_FUSED_SEAL_MAC", "0") == "1"
+# so it is off; the kernel variant stays covered by the tests, which switch it on here.
+FUSED_SEAL_MAC = False
 
 
 def seal_setup(arena: Arena, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: bytes,
