@@ -177,8 +177,8 @@ def test_one_pass_mac_block_edges(cuda, native):
     m = 433
     keys = _keytable(native, cuda, 1)
     kidx = torch.zeros(2, dtype=torch.int32, device=cuda)
-    for L in (1, 15, 16, 17, 1007, 1008, 1009, 1023, 1024, 1025, 4095, 4096, 4097, 4112, 8191,
-              16352, 16353, 32752, 32753, 65504, 65505):
+    for L in (1, 2, 15, 16, 17, 31, 32, 33, 1007, 1008, 1009, 1023, 1024, 1025, 4095, 4096, 4097, 4112, 8191,
+              4064, 4065, 8160, 8161, 16352, 16353, 16368, 32752, 32753, 49120, 49121, 65504, 65505):
         vals64 = torch.randint(0, 64, (2, L), dtype=torch.int64)
         err = torch.zeros(1, dtype=torch.int32, device=cuda)
         arena = seal(vals64.to(torch.int16).to(cuda), kidx, keys.pks, os.urandom(32), 0, err, m)
