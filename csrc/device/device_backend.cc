@@ -442,7 +442,8 @@ Keys Backend::seal_setup(Lease& mem, const Arena& a, const uint32_t* key_idx, co
                          uint64_t owner_base, const RngKeyArg& rng, uint32_t* err) {
   Keys k;
   k.keys = mem.take<MsgKey>(a.M);
-  launch_seal_setup(a.M, rng, owner_base, key_idx, pks, a.ct, a.stride, k.keys, err, nullptr, 0, s_);
+  launch_seal_setup(a.M, rng, owner_base, key_idx, pks, a.ct, a.stride, k.keys, err, nullptr, 0, nullptr,
+                    s_);
   launched("seal_setup");
   tables(mem, a, k);
   return k;

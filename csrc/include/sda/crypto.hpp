@@ -88,6 +88,11 @@ bool verify16(const uint8_t a[16], const uint8_t b[16]);
 // Returns false when the result is all-zero (libsodium crypto_scalarmult -1).
 bool x25519(uint8_t out[32], const uint8_t scalar[32], const uint8_t point[32]);
 void x25519_base(uint8_t out[32], const uint8_t scalar[32]);
+// Fixed-base table of a long-lived X25519 public key for the GPU key agreement
+// (csrc/kernels/device_crypto.hpp, x25519_base_nd): 32 x 8 entries of 32 words. False
+// (and a table of zeros) for a key on the twist, which has no edwards25519 point.
+constexpr size_t kX25519CombTableWords = 32 * 8 * 32;
+bool x25519_comb_table(uint32_t* out, const uint8_t pk[32]);
 
 // ---- Ed25519 (libsodium conventions: sk = seed || pk) ----------------------
 void ed25519_keypair_from_seed(uint8_t pk[32], uint8_t sk[64], const uint8_t seed[32]);

@@ -849,6 +849,23 @@ SDA_DEV void x25519_base(uint32_t (&out)[8], const uint32_t (&scalar)[8], const 
   x25519_base_nd(num, den, scalar, table);
   fe10_to_words(out, fe10_mul(num, fe10_invert(den)));
 }
+// The same with the recipient's key as a fixed base too: a public key that seals many
+// boxes (a clerk's, once per participant) gets its own table (host: x25519_comb_table),
+// and the shared point is 64 table additions like the public key. One loop for both
+// tables, one inversion for both results.
+SDA_DEV void x25519_seal_pair_tables(uint32_t (&epk)[8], uint32_t (&shared)[8], const uint32_t (&esk)[8],
+                                     const uint32_t* base_table, const uint32_t* key_table) {
+  Fe10 num0 = fe10_set(0), den0 = num0, num1 = num0, den1 = num0;
+#pragma unroll 1
+  for (int h = 0; h < 2; ++h) {
+    Fe10 n, d;
+    x25519_base_nd(n, d, esk, h ? key_table : base_table);
+    if (h == 0) { num0 = n; den0 = d; } else { num1 = n; den1 = d; }
+  }
+  const Fe10 inv = fe10_invert(fe10_mul(den0, den1));
+  fe10_to_words(epk, fe10_mul(num0, fe10_mul(inv, den1)));
+  fe10_to_words(shared, fe10_mul(num1, fe10_mul(inv, den0)));
+}
 // Both halves of a sealed box's key agreement, epk = esk . 9 and shared = esk . pk,
 // with one field inversion for the two (1 / (z2 den), then times the other
 // denominator). A zero z2 (a low-order pk: the shared point is rejected anyway) makes

@@ -66,10 +66,12 @@ PYBIND11_MODULE(_sda_gpu, m) {
 
   m.def("seal_setup", [](int M, std::vector<uint32_t> rng, uint64_t owner_base, uintptr_t key_idx,
                          uintptr_t pks, uintptr_t ct, uint64_t stride, uintptr_t keys,
-                         uintptr_t err, uintptr_t gate, uint32_t gate_val, uintptr_t stream) {
+                         uintptr_t err, uintptr_t gate, uint32_t gate_val, uintptr_t key_tables,
+                         uintptr_t stream) {
     launch_seal_setup(M, rng_from(rng), owner_base, P<const uint32_t>(key_idx),
                       P<const uint32_t>(pks), P<uint8_t>(ct), stride, P<MsgKey>(keys),
-                      P<uint32_t>(err), P<uint32_t>(gate), gate_val, S(stream));
+                      P<uint32_t>(err), P<uint32_t>(gate), gate_val, P<const uint32_t>(key_tables),
+                      S(stream));
     check_launch("seal_setup");
   });
   m.def("open_setup", [](int M, uintptr_t key_idx, uintptr_t sks, uintptr_t pks, uintptr_t ct,
@@ -223,6 +225,7 @@ PYBIND11_MODULE(_sda_gpu, m) {
   m.attr("SUB_BYTES") = kSubBytes;
   m.attr("SUM_TILE") = kSumTile;
   m.attr("POW_WORDS") = kPowWords;
+  m.attr("KEY_TABLE_WORDS") = kKeyTableWords;
   m.attr("POW_SHORT_WORDS") = kPowShortWords;
   m.attr("SHORT_MAX_CHUNKS") = kShortMaxChunks;
   m.def("locate_tiles", [](int M, int Sn, int L, uintptr_t pre, uintptr_t totals,

@@ -74,10 +74,14 @@ struct RngKeyArg {
 
 // ---- keys.hip --------------------------------------------------------------
 // Seal setup: esk from the device CSPRNG (purpose ephemeral, owner
-// msg_owner_base + j), epk -> header, MsgKey for encryption.
+// msg_owner_base + j), epk -> header, MsgKey for encryption. key_tables (may be null):
+// per public key a fixed-base table of kKeyTableWords words (host: x25519_comb_table; zeros
+// = none), used by the many-message form instead of the ladder.
+constexpr int kKeyTableWords = 32 * 8 * 32;
 void launch_seal_setup(int M, RngKeyArg rng, uint64_t msg_owner_base, const uint32_t* key_idx,
                        const uint32_t* pks, uint8_t* ct, uint64_t stride, MsgKey* keys,
-                       uint32_t* err, uint32_t* gate, uint32_t gate_val, hipStream_t s);
+                       uint32_t* err, uint32_t* gate, uint32_t gate_val, const uint32_t* key_tables,
+                       hipStream_t s);
 // Open setup: epk from header, X25519 with the recipient secret key.
 void launch_open_setup(int M, const uint32_t* key_idx, const uint32_t* sks, const uint32_t* pks,
                        const uint8_t* ct, uint64_t stride, MsgKey* keys, uint32_t* err,

@@ -132,7 +132,8 @@ __global__ void __launch_bounds__(kSetupBlock) k_seal_setup_many(int M, RngKeyAr
                                                         const uint32_t* __restrict__ key_idx,
                                                         const uint32_t* __restrict__ pks, uint8_t* ct,
                                                         uint64_t stride, MsgKey* keys, uint32_t* err,
-                                                        uint32_t* gate, uint32_t gate_val) {
+                                                        uint32_t* gate, uint32_t gate_val,
+                                                        const uint32_t* __restrict__ key_tables) {
   signal_dispatched(gate, gate_val);
   __builtin_amdgcn_s_setprio(3);  // see k_seal_setup
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -150,7 +151,10 @@ __global__ void __launch_bounds__(kSetupBlock) k_seal_setup_many(int M, RngKeyAr
 #pragma unroll
   for (int i = 0; i < 8; ++i) pk[i] = pkp[i];
   uint32_t epk[8], shared[8];
-  x25519_seal_pair(epk, shared, esk, pk, g_ed_base);
+  // a key with a fixed-base table of its own (word 30 of an entry marks one): no ladder
+  const uint32_t* kt = key_tables ? key_tables + (size_t)key_idx[j] * (32 * 8 * kEdEntryWords) : nullptr;
+  if (kt != nullptr && kt[30] != 0) x25519_seal_pair_tables(epk, shared, esk, g_ed_base, kt);
+  else x25519_seal_pair(epk, shared, esk, pk, g_ed_base);
   uint32_t acc = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) acc |= shared[i];
@@ -229,7 +233,8 @@ void set_key_prio(int open_prio, int powers_prio) {
 
 void launch_seal_setup(int M, RngKeyArg rng, uint64_t owner_base, const uint32_t* key_idx,
                        const uint32_t* pks, uint8_t* ct, uint64_t stride, MsgKey* keys,
-                       uint32_t* err, uint32_t* gate, uint32_t gate_val, hipStream_t s) {
+                       uint32_t* err, uint32_t* gate, uint32_t gate_val, const uint32_t* key_tables,
+                       hipStream_t s) {
   if (M <= 0) return;
   // a launch of several rounds of resident waves (~200k lanes at three ladder waves
   // per SIMD) is bound by its work, not by a ladder's latency
@@ -237,7 +242,7 @@ void launch_seal_setup(int M, RngKeyArg rng, uint64_t owner_base, const uint32_t
   if (many) {
     hipLaunchKernelGGL(k_seal_setup_many, dim3((unsigned)((M + kSetupBlock - 1) / kSetupBlock)),
                        dim3(kSetupBlock), 0, s, M, rng, owner_base, key_idx, pks, ct, stride, keys,
-                       err, gate, gate_val);
+                       err, gate, gate_val, key_tables);
     return;
   }
   const int64_t threads = 2 * (int64_t)M;

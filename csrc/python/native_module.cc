@@ -114,6 +114,18 @@ PYBIND11_MODULE(_sda_native, m) {
     crypto::x25519_base(out, U(a));
     return py::bytes(as_str(out, 32));
   });
+  c.def("x25519_comb_tables", [](std::vector<std::string> pks) {
+    // one table of kX25519CombTableWords little-endian words per key (zeros where the key
+    // has none), and which keys got one
+    std::string blob(pks.size() * crypto::kX25519CombTableWords * 4, '\0');
+    std::vector<bool> ok(pks.size());
+    for (size_t i = 0; i < pks.size(); ++i) {
+      need(pks[i], 32, "public key");
+      ok[i] = crypto::x25519_comb_table(
+          reinterpret_cast<uint32_t*>(&blob[i * crypto::kX25519CombTableWords * 4]), U(pks[i]));
+    }
+    return py::make_tuple(py::bytes(blob), ok);
+  });
   c.def("box_keypair", []() {
     uint8_t pk[32], sk[32];
     crypto::box_keypair(pk, sk);

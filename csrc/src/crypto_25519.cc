@@ -7,6 +7,7 @@
 // (client/src/crypto/signing/mod.rs:28-132). Curve constants (d, sqrt(-1), the
 // base point) are computed at start-up from their definitions.
 #include <cstring>
+#include <vector>
 
 #include "sda/crypto.hpp"
 
@@ -401,6 +402,76 @@ bool x25519(uint8_t out[32], const uint8_t scalar[32], const uint8_t point[32]) 
 void x25519_base(uint8_t out[32], const uint8_t scalar[32]) {
   uint8_t nine[32] = {9};
   x25519(out, scalar, nine);
+}
+
+// ---- fixed-base tables for X25519 with a long-lived public key -------------------
+// Entry (i, j), i < 32, j < 8, is (j + 1) 256^i P as (y + x, y - x, 2 d x y), 10 limbs of
+// 26 / 25 bits each (limb k at bit ceil(25.5 k)), padded to 32 words; word 30 of every
+// entry is 1 (a table of zeros marks a key without one). P is the edwards25519 point
+// with u = (1 + y) / (1 - y) = the key and even x (either x gives the same X25519
+// results). A key on the twist has no such point: false, and callers keep the ladder.
+namespace {
+void fe_to_limbs10(uint32_t out[10], const fe& v) {
+  uint8_t b[32];
+  fe_tobytes(b, v);
+  int bit = 0;
+  for (int k = 0; k < 10; ++k) {
+    const int w = (k & 1) ? 25 : 26;
+    uint64_t x = 0;
+    for (int q = 0; q < 5; ++q) {
+      const int idx = (bit >> 3) + q;
+      if (idx < 32) x |= (uint64_t)b[idx] << (8 * q);
+    }
+    out[k] = (uint32_t)((x >> (bit & 7)) & ((1ULL << w) - 1));
+    bit += w;
+  }
+}
+}  // namespace
+
+bool x25519_comb_table(uint32_t* out, const uint8_t pk[32]) {
+  constexpr int kEntries = 32 * 8, kWords = 32;
+  std::memset(out, 0, sizeof(uint32_t) * kEntries * kWords);
+  uint8_t ub[32];
+  std::memcpy(ub, pk, 32);
+  ub[31] &= 127;
+  const fe u = fe_frombytes(ub);
+  const fe den = fe_add(u, fe_one());
+  if (fe_iszero(den)) return false;
+  const fe y0 = fe_mul(fe_sub(u, fe_one()), fe_invert(den));
+  uint8_t enc[32];
+  fe_tobytes(enc, y0);  // sign bit clear: the even x
+  ge P;
+  if (!ge_frombytes(P, enc)) return false;
+  std::vector<ge> rows(kEntries);
+  ge base = P;
+  for (int i = 0; i < 32; ++i) {
+    ge pt = base;
+    for (int j = 0; j < 8; ++j) {
+      rows[8 * i + j] = pt;
+      pt = ge_add(pt, base);
+    }
+    for (int q = 0; q < 8; ++q) base = ge_dbl(base);
+  }
+  // one inversion for all 256 denominators
+  std::vector<fe> pref(kEntries);
+  fe acc = fe_one();
+  for (int e = 0; e < kEntries; ++e) {
+    pref[e] = acc;
+    acc = fe_mul(acc, rows[e].Z);
+  }
+  fe inv = fe_invert(acc);
+  const fe d2 = K().d2;
+  for (int e = kEntries - 1; e >= 0; --e) {
+    const fe zi = fe_mul(inv, pref[e]);
+    inv = fe_mul(inv, rows[e].Z);
+    const fe x = fe_mul(rows[e].X, zi), y = fe_mul(rows[e].Y, zi);
+    uint32_t* w = out + (size_t)e * kWords;
+    fe_to_limbs10(w, fe_add(y, x));
+    fe_to_limbs10(w + 10, fe_sub(y, x));
+    fe_to_limbs10(w + 20, fe_mul(fe_mul(x, y), d2));
+    w[30] = 1;
+  }
+  return true;
 }
 
 // ---- Ed25519 -----------------------------------------------------------------

@@ -107,6 +107,23 @@ class KeyTable:
     def holds(self, i: int) -> bool:
         return self.sk_bytes[i] is not None
 
+    # launches of at least this many boxes use the keys' fixed-base tables (the
+    # many-message form of the seal-side key agreement, keys.hip)
+    TABLE_MIN_BOXES = 65536
+
+    def tables(self, boxes: int | None = None):
+        """Fixed-base tables of the public keys (int32 [K][KEY_TABLE_WORDS], built on
+        the host once and kept): with them a sealed box's shared point costs 64 table
+        additions instead of a 255-step ladder. None below `TABLE_MIN_BOXES` boxes, where
+        the launch is latency-bound and the two-ladder kernel runs anyway."""
+        if boxes is not None and boxes < self.TABLE_MIN_BOXES:
+            return None
+        if getattr(self, "_tables", None) is None:
+            blob, _ok = native().crypto.x25519_comb_tables(list(self.pk_bytes))
+            t = torch.frombuffer(bytearray(blob), dtype=torch.int32)
+            self._tables = t.view(len(self.pk_bytes), G.KEY_TABLE_WORDS).to(self.pks.device)
+        return self._tables
+
     @classmethod
     def generate(cls, count: int, device) -> "KeyTable":
         c = native().crypto
@@ -387,8 +404,8 @@ class DeviceAggregator:
         side.wait_stream(main)
         with torch.cuda.stream(side):
             # Poly1305 tables on the side stream too: the encrypt is ~3 ms away
-            ks_clerk = seal_setup(clerk_arena, kidx_clerk, pks, rng_key, 0, err,
-                                  gate=gate).with_powers()
+            ks_clerk = seal_setup(clerk_arena, kidx_clerk, pks, rng_key, 0, err, gate=gate,
+                                  pk_tables=self.keys.tables(n * P)).with_powers()
             ks_mask = (seal_setup(mask_arena, kidx_rcpt_p, pks, rng_key, n * P, err).with_powers()
                        if mask_arena is not None else None)
             ev_sealkeys = torch.cuda.Event()

@@ -95,18 +95,27 @@ def _gate_args(gate):
     return _ptr(t), int(v) & 0xFFFFFFFF
 
 
-def seal_setup(M, rng_key, owner_base, key_idx, pks, ct, stride, keys, err, gate=None):
+KEY_TABLE_WORDS = 32 * 8 * 32  # fixed-base table of one public key (kernels.hpp kKeyTableWords)
+
+
+def seal_setup(M, rng_key, owner_base, key_idx, pks, ct, stride, keys, err, gate=None,
+               pk_tables=None):
+    """`pk_tables` (int32 [K][KEY_TABLE_WORDS], from the host's x25519_comb_tables): the
+    public keys' fixed-base tables, which large launches use instead of the ladder."""
     _check(key_idx, "key_idx", torch.int32, numel=M)
     _check(pks, "pks", torch.int32)
     if pks.numel() % 8:
         raise ValueError("pks must be [K][8] words")
+    if pk_tables is not None:
+        _check(pk_tables, "pk_tables", torch.int32, numel=pks.numel() // 8 * KEY_TABLE_WORDS)
     _check(ct, "ct", torch.uint8, min_numel=M * stride)
     _check(keys, "keys", torch.uint8, min_numel=M * MSGKEY_BYTES)
     _check(err, "err", torch.int32, numel=1)
     if stride % 64:
         raise ValueError("stride must be a multiple of 64")
     _gpu().seal_setup(M, rng_words(rng_key), owner_base, _ptr(key_idx), _ptr(pks), _ptr(ct),
-                      stride, _ptr(keys), _ptr(err), *_gate_args(gate), _stream())
+                      stride, _ptr(keys), _ptr(err), *_gate_args(gate),
+                      0 if pk_tables is None else _ptr(pk_tables), _stream())
 
 
 def open_setup(M, key_idx, sks, pks, ct, stride, keys, err, gate=None):

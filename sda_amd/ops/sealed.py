@@ -160,7 +160,7 @@ FUSED_SEAL_MAC = False
 
 
 def seal_setup(arena: Arena, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: bytes,
-               owner_base: int, err: torch.Tensor, gate=None) -> KeySet:
+               owner_base: int, err: torch.Tensor, gate=None, pk_tables=None) -> KeySet:
     """Ephemeral keypairs + X25519 + nonce/subkey derivation for every slot.
 
     Independent of the message contents, so the engine runs it on a side stream
@@ -172,7 +172,7 @@ def seal_setup(arena: Arena, key_idx: torch.Tensor, pks: torch.Tensor, rng_key: 
     """
     keys = torch.empty(arena.M * G.MSGKEY_BYTES, dtype=torch.uint8, device=arena.ct.device)
     G.seal_setup(arena.M, rng_key, owner_base, key_idx, pks, arena.ct, arena.stride, keys, err,
-                 gate=gate)
+                 gate=gate, pk_tables=pk_tables)
     return KeySet(arena.M, keys, None, arena.K)
 
 

@@ -238,7 +238,8 @@ class DeviceCommittee:
         gate = eng._gate_token()
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            ks = seal_setup(arena, kidx_send, pks, rng_key, 0, err, gate=gate).with_powers()
+            ks = seal_setup(arena, kidx_send, pks, rng_key, 0, err, gate=gate,
+                            pk_tables=eng.keys.tables(arena.M)).with_powers()
             ks_mask = None
             if mask_arena is not None:
                 ks_mask = seal_setup(mask_arena, kidx_rcpt, pks, rng_key, n * P, err).with_powers()

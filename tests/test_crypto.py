@@ -167,3 +167,31 @@ def test_openssl_oracle_x25519_ed25519(native):
         seed = os.urandom(32)
         pk, _ = native.crypto.ed25519_keypair_from_seed(seed)
         assert pk == _evp_raw_public(lib, NID_ED25519, seed)
+
+
+def test_x25519_comb_table_of_the_base_point_is_the_generated_one(native):
+    """The host's fixed-base table builder (Montgomery u -> edwards25519 point, 32 x 8
+    multiples, one inversion for all) on u = 9 gives the table the GPU's ephemeral
+    public keys come from (csrc/kernels/ed25519_base.inc, written by
+    scripts/gen_ed25519_base.py with plain integers)."""
+    import os
+    import re
+    import struct
+
+    blob, ok = native.crypto.x25519_comb_tables([bytes([9] + [0] * 31)])
+    assert ok == [True]
+    words = struct.unpack("<%dI" % (len(blob) // 4), blob)
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "kernels",
+                       "ed25519_base.inc")
+    ref = [int(x, 16) for x in re.findall(r"0x([0-9a-f]+)u", open(inc).read())]
+    assert len(ref) == len(words) == 32 * 8 * 32
+    for e in range(256):
+        assert list(words[32 * e:32 * e + 30]) == ref[32 * e:32 * e + 30], e
+        assert words[32 * e + 30] == 1  # the "has a table" mark
+
+
+def test_x25519_comb_table_refuses_a_key_on_the_twist(native):
+    # u = 2 is not the u-coordinate of a curve25519 point (it lies on the twist)
+    blob, ok = native.crypto.x25519_comb_tables([bytes([2] + [0] * 31), native.crypto.box_keypair()[0]])
+    assert ok == [False, True]
+    assert blob[:32 * 8 * 32 * 4] == bytes(32 * 8 * 32 * 4)

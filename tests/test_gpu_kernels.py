@@ -60,26 +60,41 @@ def test_x25519_fixed_base_matches_ladder(cuda, native):
         assert b[j].cpu().numpy().tobytes() == host
 
 
-@pytest.mark.parametrize("many", [0, 1])
-def test_seal_setup_forms_open_on_host(cuda, native, many):
-    """Both key-agreement kernels of the seal side -- two lanes per message with two
-    ladders, one lane with the fixed-base table -- give boxes the host opens."""
+@pytest.mark.parametrize("many,tables", [(0, False), (1, False), (1, True)])
+def test_seal_setup_forms_open_on_host(cuda, native, many, tables):
+    """The key-agreement kernels of the seal side -- two lanes per message with two
+    ladders; one lane with the fixed-base table for the public key and a ladder for the
+    shared point; one lane with tables for both (the recipients' keys get their own,
+    one of them a key on the twist that has none) -- give boxes the host opens."""
     from sda_amd._native import gpu
-    from sda_amd.ops.sealed import seal
+    from sda_amd.engine import KeyTable
+    from sda_amd.ops.sealed import Arena, seal_data, seal_setup
     keys = _keytable(native, cuda, 2)
+    if tables:
+        assert keys.tables(10) is None and keys.tables(10 ** 6) is not None
+        # a third recipient whose public key is on the twist (no edwards25519 point):
+        # X25519 still works for it, through the ladder
+        sk3 = os.urandom(32)
+        keys = KeyTable.from_bytes(keys.pk_bytes + [bytes([2] + [0] * 31)], keys.sk_bytes + [sk3], cuda)
     M, L, m = 70, 300, 433
+    nk = len(keys.pk_bytes)
     vals64 = torch.randint(0, m, (M, L), dtype=torch.int64)
-    kidx = torch.tensor([j % 2 for j in range(M)], dtype=torch.int32, device=cuda)
+    kidx = torch.tensor([j % nk for j in range(M)], dtype=torch.int32, device=cuda)
     err = torch.zeros(1, dtype=torch.int32, device=cuda)
     gpu().set_seal_many(many)
     try:
-        arena = seal(vals64.to(torch.int16).to(cuda), kidx, keys.pks, os.urandom(32), 0, err, m)
+        arena = Arena.empty(M, L, m, cuda)
+        ks = seal_setup(arena, kidx, keys.pks, os.urandom(32), 0, err,
+                        pk_tables=keys.tables() if tables else None)
+        seal_data(arena, ks, vals64.to(torch.int16).to(cuda), err)
         blobs = arena.to_blobs()
     finally:
         gpu().set_seal_many(-1)
     assert int(err.item()) == 0
     for j in range(M):
-        pt = native.crypto.box_seal_open(blobs[j], keys.pk_bytes[j % 2], keys.sk_bytes[j % 2])
+        if j % nk == 2:  # the twist key has no matching secret key: its boxes only have to be
+            continue     # produced without an error (the ladder path beside the table path)
+        pt = native.crypto.box_seal_open(blobs[j], keys.pk_bytes[j % nk], keys.sk_bytes[j % nk])
         assert pt is not None and varint_decode(pt) == vals64[j].tolist(), j
 
 
