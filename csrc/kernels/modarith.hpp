@@ -68,6 +68,16 @@ struct ModF64 {
   double m, inv;
 };
 inline ModF64 make_modf64(uint32_t m) { return ModF64{(double)m, m ? 1.0 / (double)m : 0.0}; }
+// v given as a double (an exact integer below 2^53)
+SDA_DEV uint32_t modf64d(double vd, const ModF64& P) {
+  const double q = __builtin_trunc(vd * P.inv);
+  int32_t r = (int32_t)__builtin_fma(-q, P.m, vd);  // in (-m, 2m)
+  const int32_t m = (int32_t)P.m;
+  r += (r >> 31) & m;
+  r -= m;
+  r += (r >> 31) & m;
+  return (uint32_t)r;
+}
 SDA_DEV uint32_t modf64(uint64_t v, const ModF64& P) {
   const double vd = (double)(int64_t)v;
   const double q = __builtin_trunc(vd * P.inv);

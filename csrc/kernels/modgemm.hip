@@ -39,6 +39,7 @@
 // row, summed over the 16 lanes of a row group on the VALU (DPP), one atomic add
 // per (row, wave) -- instead of a second pass over the stored shares.
 #include <algorithm>
+#include <type_traits>
 
 #include "block_utils.hpp"
 #include "device_crypto.hpp"
@@ -64,6 +65,110 @@ SDA_DEV int swz(int row, int chunk) {  // position of a row's 16-byte chunk insi
 // Horner chain of 32-bit Barrett steps (p < 2^24: s < p and acc_d < 2^31 keep
 // s * 2^7 + acc_d below 2^32). 2: 64-bit multiply-adds by 2^(7d) mod p and one 64-bit
 // Barrett reduction (any p < 2^28). 0 and 2 are the integer-only references.
+//
+// Epilogue of one 64 x 128 block tile held as degree sums in `acc` (wave (wm, wn) of the
+// 2 x 2, C/D map of the 16x16 MFMA): fold, store, and -- with `cnt` -- the byte counts.
+template <typename VT, int kLimbs, int kFold>
+__device__ __forceinline__ void gemm_epilogue(const v4i (&acc)[2][4][2 * kLimbs - 1], int m_blk, int n_blk,
+                                              int z, int wm, int wn, int lane, int M, int N, int batches,
+                                              const ModParams& mp, const ModF64& mf, VT* __restrict__ C,
+                                              int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit,
+                                              uint32_t* __restrict__ cnt, int cnt_tiles) {
+  constexpr int kDeg = 2 * kLimbs - 1;
+  // epilogue: C/D map col = lane & 15, row = 4*(lane >> 4) + r. Output indices are
+  // built from per-lane bases by additions (the general z/m/n strides would cost
+  // three 64-bit multiplies per element otherwise).
+  uint32_t w[kDeg];
+  if constexpr (kFold == 2) {
+#pragma unroll
+    for (int d = 0; d < kDeg; ++d) w[d] = (uint32_t)(((uint64_t)1 << (kLimbBits * d)) % mp.m);
+  }
+  const int row0 = m_blk + wm * 32 + 4 * (lane >> 4);
+  const int col0 = n_blk + wn * 64 + (lane & 15);
+  const int64_t base = (int64_t)z * ldc_z + (int64_t)row0 * ldc_m + (int64_t)col0 * ldc_n;
+  const int64_t step_j = 16 * ldc_n, step_i = 16 * ldc_m;
+  uint32_t bytes[2][2] = {{0, 0}, {0, 0}};  // varint bytes of rows (i, r): two 16-bit sums per word
+  // A block whose whole tile is inside the matrix and below `limit` (nine in ten of the
+  // share GEMMs' blocks) stores without any per-element test: the tests are a compare
+  // or two and a branch per element otherwise.
+  const bool inside = m_blk + kBM <= M && n_blk + kBN <= N && limit < 0;  // block-uniform
+  auto tile_out = [&](auto interior) {
+    constexpr bool kInterior = decltype(interior)::value;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = row0 + 16 * i + r;
+      if (!kInterior && row >= M) continue;
+      int64_t idx = base + i * step_i + r * ldc_m;
+#pragma unroll
+      for (int j = 0; j < 4; ++j, idx += step_j) {
+        if (!kInterior && col0 + 16 * j >= N) continue;
+        uint32_t out;
+        if constexpr (kFold == 1) {
+          // neighbouring degrees pair up in 32 bits (acc_d 2^7 + acc_(d-1) < 2^32: the
+          // caller's bound on K), the pairs meet as doubles: exact integers below 2^53
+          auto pair = [&](int d) -> double {  // acc_(d+1) 2^7 + acc_d, or acc_d alone at the top
+            uint32_t v = (uint32_t)acc[i][j][d][r];
+            if (d + 1 < kDeg) v += (uint32_t)acc[i][j][d + 1][r] << kLimbBits;
+            return (double)v;
+          };
+          if constexpr (kLimbs == 3) {
+            const double s = __builtin_fma(pair(4), 268435456.0, __builtin_fma(pair(2), 16384.0, pair(0)));
+            out = modf64d(s, mf);
+          } else {
+            // degrees 4..6 first (below 2^46), reduced; then with the low four (below 2^53)
+            const double hi = __builtin_fma(pair(6), 16384.0, pair(4));
+            const double rh = (double)modf64d(hi, mf);
+            const double s = __builtin_fma(rh, 268435456.0, __builtin_fma(pair(2), 16384.0, pair(0)));
+            out = modf64d(s, mf);
+          }
+        } else if constexpr (kFold == 0) {
+          // acc_d < 2^31, s < p < 2^24: s * 2^7 + acc_d < 2^32
+          uint32_t s = mod32((uint32_t)acc[i][j][kDeg - 1][r], mp);
+#pragma unroll
+          for (int d = kDeg - 2; d >= 0; --d) s = mod32((s << kLimbBits) + (uint32_t)acc[i][j][d][r], mp);
+          out = s;
+        } else {
+          uint64_t s = 0;
+#pragma unroll
+          for (int d = 0; d < kDeg; ++d)
+            s += (uint64_t)mod32((uint32_t)acc[i][j][d][r], mp) * w[d];  // < 7 * 2^56
+          out = mod64(s, mp);
+        }
+        if (kInterior || limit < 0 || idx < limit) {  // limit < 0: every in-range element is stored
+          C[idx] = (VT)out;
+          // zigzag code 2 * out: one byte below 2^6, two below 2^13, ...
+          uint32_t len = 1u + (out >= (1u << 6)) + (out >= (1u << 13)) + (out >= (1u << 20));
+          if constexpr (kLimbs > 3) len += out >= (1u << 27);
+          bytes[i][r >> 1] += len << (16 * (r & 1));
+        }
+      }
+    }
+  };
+  if (inside) tile_out(std::true_type{});
+  else tile_out(std::false_type{});
+  if (cnt == nullptr) return;  // uniform
+  // the block's 128 columns lie inside one count tile (kTileValues is a multiple of kBN)
+  static_assert(kTileValues % kBN == 0, "a block's columns must not straddle a count tile");
+  const int tile = n_blk / kTileValues;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // a row's 64 columns of this wave: 4 per lane, over the 16 lanes of the row group
+      const uint32_t sum = row16_incl_scan(bytes[i][h]);
+      if ((lane & 15) != 15) continue;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int row = row0 + 16 * i + 2 * h + q;
+        const uint32_t v = (sum >> (16 * q)) & 0xffffu;
+        if (row < M && v != 0)
+          atomicAdd(&cnt[((int64_t)row * batches + z) * cnt_tiles + tile], v);
+      }
+    }
+}
+
 // Block id -> tile. K is short, so the kernel lives on operand reuse between blocks: a
 // column panel of B (128 columns of one batch) is read by every row block, a row block
 // of A by every panel. Consecutive block ids go round the 8 XCDs, each with its own
@@ -182,84 +287,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     if (ks + 1 < nk) commit(cur ^ 1);
     __syncthreads();
   }
-  // epilogue: C/D map col = lane & 15, row = 4*(lane >> 4) + r. Output indices are
-  // built from per-lane bases by additions (the general z/m/n strides would cost
-  // three 64-bit multiplies per element otherwise).
-  uint32_t w[kDeg];
-  if constexpr (kFold == 2) {
-#pragma unroll
-    for (int d = 0; d < kDeg; ++d) w[d] = (uint32_t)(((uint64_t)1 << (kLimbBits * d)) % mp.m);
-  }
-  const int row0 = m_blk + wm * 32 + 4 * (lane >> 4);
-  const int col0 = n_blk + wn * 64 + (lane & 15);
-  const int64_t base = (int64_t)z * ldc_z + (int64_t)row0 * ldc_m + (int64_t)col0 * ldc_n;
-  const int64_t step_j = 16 * ldc_n, step_i = 16 * ldc_m;
-  uint32_t bytes[2][2] = {{0, 0}, {0, 0}};  // varint bytes of rows (i, r): two 16-bit sums per word
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = row0 + 16 * i + r;
-      if (row >= M) continue;
-      int64_t idx = base + i * step_i + r * ldc_m;
-#pragma unroll
-      for (int j = 0; j < 4; ++j, idx += step_j) {
-        if (col0 + 16 * j >= N) continue;
-        uint32_t out;
-        if constexpr (kFold == 1) {
-          constexpr int kSplit = kLimbs == 3 ? 0 : 3;  // degrees >= kSplit are folded first
-          uint64_t hi = 0;
-          if constexpr (kSplit > 0) {
-#pragma unroll
-            for (int d = kDeg - 1; d >= kSplit; --d)
-              hi += (uint64_t)(uint32_t)acc[i][j][d][r] << (kLimbBits * (d - kSplit));
-            hi = (uint64_t)modf64(hi, mf) << (kLimbBits * kSplit);
-          }
-#pragma unroll
-          for (int d = (kSplit > 0 ? kSplit : kDeg) - 1; d >= 0; --d)
-            hi += (uint64_t)(uint32_t)acc[i][j][d][r] << (kLimbBits * d);
-          out = modf64(hi, mf);
-        } else if constexpr (kFold == 0) {
-          // acc_d < 2^31, s < p < 2^24: s * 2^7 + acc_d < 2^32
-          uint32_t s = mod32((uint32_t)acc[i][j][kDeg - 1][r], mp);
-#pragma unroll
-          for (int d = kDeg - 2; d >= 0; --d) s = mod32((s << kLimbBits) + (uint32_t)acc[i][j][d][r], mp);
-          out = s;
-        } else {
-          uint64_t s = 0;
-#pragma unroll
-          for (int d = 0; d < kDeg; ++d)
-            s += (uint64_t)mod32((uint32_t)acc[i][j][d][r], mp) * w[d];  // < 7 * 2^56
-          out = mod64(s, mp);
-        }
-        if (idx < limit) {
-          C[idx] = (VT)out;
-          // zigzag code 2 * out: one byte below 2^6, two below 2^13, ...
-          uint32_t len = 1u + (out >= (1u << 6)) + (out >= (1u << 13)) + (out >= (1u << 20));
-          if constexpr (kLimbs > 3) len += out >= (1u << 27);
-          bytes[i][r >> 1] += len << (16 * (r & 1));
-        }
-      }
-    }
-  if (cnt == nullptr) return;  // uniform
-  // the block's 128 columns lie inside one count tile (kTileValues is a multiple of kBN)
-  static_assert(kTileValues % kBN == 0, "a block's columns must not straddle a count tile");
-  const int tile = n_blk / kTileValues;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      // a row's 64 columns of this wave: 4 per lane, over the 16 lanes of the row group
-      const uint32_t sum = row16_incl_scan(bytes[i][h]);
-      if ((lane & 15) != 15) continue;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int row = row0 + 16 * i + 2 * h + q;
-        const uint32_t v = (sum >> (16 * q)) & 0xffffu;
-        if (row < M && v != 0)
-          atomicAdd(&cnt[((int64_t)row * batches + z) * cnt_tiles + tile], v);
-      }
-    }
+  gemm_epilogue<VT, kLimbs, kFold>(acc, m_blk, n_blk, z, wm, wn, lane, M, N, batches, mp, mf, C, ldc_z,
+                                   ldc_m, ldc_n, limit, cnt, cnt_tiles);
 }
 
 template <int kLimbs>
@@ -342,7 +371,7 @@ __global__ void __launch_bounds__(256)
 
 }  // namespace
 
-static int g_gemm_fold_f64 = 1;  // 0 never, 1 three-limb fields (default), 2 four-limb ones too
+static int g_gemm_fold_f64 = 2;  // 0 never, 1 three-limb fields only, 2 every field below 2^24 (default)
 void set_gemm_fold_f64(int mode) { g_gemm_fold_f64 = mode; }
 
 void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p, const int8_t* A,
@@ -351,13 +380,19 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
   if (M <= 0 || N <= 0 || batches <= 0) return;
   ModParams mp = make_mod_params(p);
   const ModF64 mf = make_modf64(p);
+  // no truncation: the per-element bound check goes away (the kernel takes limit < 0)
+  if ((int64_t)(batches - 1) * ldc_z + (int64_t)(M - 1) * ldc_m + (int64_t)(N - 1) * ldc_n < limit &&
+      ldc_z >= 0 && ldc_m >= 0 && ldc_n >= 0)
+    limit = -1;
   // three limbs fold all five degrees in one 64-bit sum: acc_d <= Kp 127^2 min(d + 1, 5 - d)
-  const bool fits53 = limbs == 4 || (uint64_t)Kp * 127 * 127 * ((1ull << 28) + (2ull << 21) + (3ull << 14) +
-                                                               (2ull << 7) + 1) < (1ull << 53);
-  // measured on the share GEMMs of the two large reference fields: three limbs 29.6 ->
-  // 28.5 ms with the double-precision fold, four limbs 25.6 -> 27.6 ms (its two-stage
-  // fold spills next to 224 accumulator registers): default for three limbs only
-  const bool f64 = g_gemm_fold_f64 == 2 || (g_gemm_fold_f64 == 1 && limbs == 3);
+  // and the 32-bit pairs: (acc_(d+1) << 7) + acc_d with at most `limbs` products per degree
+  const bool fits53 = (limbs == 4 || (uint64_t)Kp * 127 * 127 * ((1ull << 28) + (2ull << 21) + (3ull << 14) +
+                                                                (2ull << 7) + 1) < (1ull << 53)) &&
+                      (uint64_t)Kp * 127 * 127 * limbs * 129 < (1ull << 32);
+  // measured on the share GEMMs of the two large reference fields, against the Horner
+  // chain: three limbs 28.9 -> 27.8 ms, four limbs 21.0 -> 20.4 ms (four limbs: the
+  // second stage's r 2^28 + ... stays below 2^53 only for p < 2^24)
+  const bool f64 = (g_gemm_fold_f64 == 2 && p < (1u << 24)) || (g_gemm_fold_f64 == 1 && limbs == 3);
   const int fold = f64 && fits53 ? 1 : (p >= (1u << 24) ? 2 : 0);
   GemmGrid gg;
   gg.gx = (N + kBN - 1) / kBN;
