@@ -260,6 +260,7 @@ PYBIND11_MODULE(_sda_gpu, m) {
     check_launch("x25519_base");
   });
   m.def("set_gemm_fold_f64", &set_gemm_fold_f64);
+  m.def("set_gemm_panel", &set_gemm_panel);
   m.def("colsum", [](int G, int R, int L, uint32_t mod, int value_bytes, uintptr_t vals,
                      uintptr_t out, uintptr_t stream) {
     launch_colsum(G, R, L, mod, value_bytes, P<const void>(vals), P<uint32_t>(out), S(stream));

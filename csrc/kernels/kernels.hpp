@@ -254,6 +254,8 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
 // epilogue fold through the double-precision unit: 0 never (integer only), 1 for
 // three-limb fields (default), 2 for four-limb fields too
 void set_gemm_fold_f64(int mode);
+// -1 (default): the panel-resident kernel for short K with at least four row blocks; 0 never; 1 whenever Kp <= 256
+void set_gemm_panel(int mode);
 // X limbs [3][P][B][Kp] of packed-Shamir inputs: secrets (canonical) then t draws.
 void launch_pss_x_limbs(int P, int D, int B, int k, int t, int Kp, int limbs, uint32_t p,
                         const int32_t* secrets, RngKeyArg rng, uint64_t owner_base, int8_t* X,

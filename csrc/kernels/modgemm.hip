@@ -66,10 +66,11 @@ SDA_DEV int swz(int row, int chunk) {  // position of a row's 16-byte chunk insi
 // s * 2^7 + acc_d below 2^32). 2: 64-bit multiply-adds by 2^(7d) mod p and one 64-bit
 // Barrett reduction (any p < 2^28). 0 and 2 are the integer-only references.
 //
-// Epilogue of one 64 x 128 block tile held as degree sums in `acc` (wave (wm, wn) of the
-// 2 x 2, C/D map of the 16x16 MFMA): fold, store, and -- with `cnt` -- the byte counts.
-template <typename VT, int kLimbs, int kFold>
-__device__ __forceinline__ void gemm_epilogue(const v4i (&acc)[2][4][2 * kLimbs - 1], int m_blk, int n_blk,
+// Epilogue of a wave's 32 x 16 kJT outputs held as degree sums in `acc` (rows from
+// m_blk + 32 wm, columns from n_blk + 16 kJT wn, C/D map of the 16x16 MFMA): fold,
+// store, and -- with `cnt` -- the byte counts.
+template <typename VT, int kLimbs, int kFold, int kJT>
+__device__ __forceinline__ void gemm_epilogue(const v4i (&acc)[2][kJT][2 * kLimbs - 1], int m_blk, int n_blk,
                                               int z, int wm, int wn, int lane, int M, int N, int batches,
                                               const ModParams& mp, const ModF64& mf, VT* __restrict__ C,
                                               int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit,
@@ -84,7 +85,7 @@ __device__ __forceinline__ void gemm_epilogue(const v4i (&acc)[2][4][2 * kLimbs 
     for (int d = 0; d < kDeg; ++d) w[d] = (uint32_t)(((uint64_t)1 << (kLimbBits * d)) % mp.m);
   }
   const int row0 = m_blk + wm * 32 + 4 * (lane >> 4);
-  const int col0 = n_blk + wn * 64 + (lane & 15);
+  const int col0 = n_blk + wn * (16 * kJT) + (lane & 15);
   const int64_t base = (int64_t)z * ldc_z + (int64_t)row0 * ldc_m + (int64_t)col0 * ldc_n;
   const int64_t step_j = 16 * ldc_n, step_i = 16 * ldc_m;
   uint32_t bytes[2][2] = {{0, 0}, {0, 0}};  // varint bytes of rows (i, r): two 16-bit sums per word
@@ -102,7 +103,7 @@ __device__ __forceinline__ void gemm_epilogue(const v4i (&acc)[2][4][2 * kLimbs 
       if (!kInterior && row >= M) continue;
       int64_t idx = base + i * step_i + r * ldc_m;
 #pragma unroll
-      for (int j = 0; j < 4; ++j, idx += step_j) {
+      for (int j = 0; j < kJT; ++j, idx += step_j) {
         if (!kInterior && col0 + 16 * j >= N) continue;
         uint32_t out;
         if constexpr (kFold == 1) {
@@ -156,7 +157,7 @@ __device__ __forceinline__ void gemm_epilogue(const v4i (&acc)[2][4][2 * kLimbs 
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      // a row's 64 columns of this wave: 4 per lane, over the 16 lanes of the row group
+      // a row's columns of this wave: kJT per lane, over the 16 lanes of the row group
       const uint32_t sum = row16_incl_scan(bytes[i][h]);
       if ((lane & 15) != 15) continue;
 #pragma unroll
@@ -287,8 +288,121 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     if (ks + 1 < nk) commit(cur ^ 1);
     __syncthreads();
   }
-  gemm_epilogue<VT, kLimbs, kFold>(acc, m_blk, n_blk, z, wm, wn, lane, M, N, batches, mp, mf, C, ldc_z,
-                                   ldc_m, ldc_n, limit, cnt, cnt_tiles);
+  gemm_epilogue<VT, kLimbs, kFold, 4>(acc, m_blk, n_blk, z, wm, wn, lane, M, N, batches, mp, mf, C, ldc_z,
+                                      ldc_m, ldc_n, limit, cnt, cnt_tiles);
+}
+
+// The same product for short K (Kp <= 256: share generation, K = t + k), one workgroup
+// per column panel of B. The general kernel above restages its B panel for every row
+// block, and its waves meet at a barrier every K-step, so the MFMAs of a tile and the
+// epilogue of the tile before it rarely overlap: measured, a tile took 15.8k cycles of
+// a SIMD for 4.6k cycles of MFMAs and about as many of other instructions. Here the
+// panel's limbs (128 columns x Kp x L bytes, 96 / 128 KB) are loaded into LDS once and
+// the workgroup walks down all row blocks of A against them. A is small and shared by
+// every panel (it stays in each XCD's L2), so each wave loads its own A fragments
+// straight from global memory in the MFMA operand layout -- lane (r, g) takes bytes
+// [16 g, 16 g + 16) of row r of the K-step -- one step ahead of the MFMAs that use
+// them. After the panel is in LDS nothing is written to it and no wave waits for
+// another: the two waves of a SIMD drift apart, and one's epilogue fills the issue
+// slots under the other's MFMAs.
+// Eight waves: with three limbs two teams of 2 x 2 waves (32 x 64 outputs per wave, 120
+// accumulator registers) take alternate row blocks; with four limbs one team of 2 x 4
+// (32 x 32 per wave, 112 registers).
+constexpr int kPanelMaxK = 256;
+
+template <typename VT, int kLimbs, int kFold>
+__global__ void __launch_bounds__(512)
+    k_modgemm_panel(int M, int N, int Kp, int batches, int gx, int gy, ModParams mp, ModF64 mf,
+                    const int8_t* __restrict__ A, const int8_t* __restrict__ B, int64_t b_batch,
+                    VT* __restrict__ C, int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit,
+                    uint32_t* __restrict__ cnt, int cnt_tiles) {
+  constexpr int kDeg = 2 * kLimbs - 1;
+  constexpr int kTeams = kLimbs == 3 ? 2 : 1;
+  constexpr int kJT = kLimbs == 3 ? 4 : 2;  // 16-column tiles per wave
+  constexpr int kSteps = kPanelMaxK / kBK;
+  constexpr int kPlane = kBN * kBK;         // one (limb, K-step) slab of the panel
+  __shared__ __attribute__((aligned(16))) int8_t Bs[kLimbs * kSteps * kPlane];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int team = kTeams == 2 ? wave >> 2 : 0;
+  const int wm = kTeams == 2 ? (wave >> 1) & 1 : wave >> 2;
+  const int wn = kTeams == 2 ? wave & 1 : wave & 3;
+  const int n_blk = ((int)blockIdx.x % gx) * kBN, z = (int)blockIdx.x / gx;
+  const int nk = Kp / kBK;
+  {
+    // the panel: rows = columns of C, 16-byte pieces; 16 consecutive threads take one
+    // row's Kp bytes. All loads are issued before the first LDS write.
+    const int8_t* Bz = B + (int64_t)z * (int64_t)N * Kp;
+    const int cpr = Kp / 16, pieces = kLimbs * kBN * cpr;
+    constexpr int kMine = kLimbs * kBN * (kPanelMaxK / 16) / 512;
+    v4i t[kMine];
+    int dst[kMine];
+#pragma unroll
+    for (int u = 0; u < kMine; ++u) {
+      const int id = u * 512 + tid;
+      const int c = id % cpr, rl = id / cpr, row = rl % kBN, l = rl / kBN;
+      const int grow = n_blk + row;
+      const bool ok = id < pieces;
+      dst[u] = ok ? ((l * kSteps + (c >> 2)) * kBN + row) * kBK + 16 * swz(row, c & 3) : -1;
+      t[u] = ok && grow < N ? *reinterpret_cast<const v4i*>(Bz + l * b_batch + (int64_t)grow * Kp + 16 * c)
+                            : v4i{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < kMine; ++u)
+      if (dst[u] >= 0) *reinterpret_cast<v4i*>(Bs + dst[u]) = t[u];
+  }
+  __syncthreads();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int b_off = (wn * (16 * kJT) + fr) * kBK + 16 * swz(fr, fg);
+  const int64_t a_plane = (int64_t)M * Kp;
+  // rows past M read row M - 1: their outputs are never stored
+  auto load_a = [&](v4i (&f)[2][kLimbs], int mb, int ks) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = min(mb * kBM + wm * 32 + 16 * i + fr, M - 1);
+      const int8_t* p = A + (int64_t)row * Kp + ks * kBK + 16 * fg;
+#pragma unroll
+      for (int l = 0; l < kLimbs; ++l) f[i][l] = *reinterpret_cast<const v4i*>(p + l * a_plane);
+    }
+  };
+  v4i fa[2][kLimbs], fnext[2][kLimbs];
+  if (team < gy) load_a(fa, team, 0);
+  for (int mb = team; mb < gy; mb += kTeams) {
+    v4i acc[2][kJT][kDeg];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < kJT; ++j)
+#pragma unroll
+        for (int d = 0; d < kDeg; ++d) acc[i][j][d] = v4i{0, 0, 0, 0};
+    for (int ks = 0; ks < nk; ++ks) {
+      const bool more = ks + 1 < nk;
+      const int nmb = more ? mb : mb + kTeams;
+      if (nmb < gy) load_a(fnext, nmb, more ? ks + 1 : 0);
+      const int8_t* base = Bs + ks * kPlane + b_off;
+#pragma unroll
+      for (int j = 0; j < kJT; ++j) {
+        v4i fb[kLimbs];
+#pragma unroll
+        for (int l = 0; l < kLimbs; ++l)
+          fb[l] = *reinterpret_cast<const v4i*>(base + l * kSteps * kPlane + 16 * j * kBK);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int la = 0; la < kLimbs; ++la)
+#pragma unroll
+            for (int lb = 0; lb < kLimbs; ++lb)
+              acc[i][j][la + lb] =
+                  __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i][la], fb[lb], acc[i][j][la + lb], 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int l = 0; l < kLimbs; ++l) fa[i][l] = fnext[i][l];
+    }
+    gemm_epilogue<VT, kLimbs, kFold, kJT>(acc, mb * kBM, n_blk, z, wm, wn, lane, M, N, batches, mp, mf, C,
+                                          ldc_z, ldc_m, ldc_n, limit, cnt, cnt_tiles);
+  }
 }
 
 template <int kLimbs>
@@ -373,6 +487,8 @@ __global__ void __launch_bounds__(256)
 
 static int g_gemm_fold_f64 = 2;  // 0 never, 1 three-limb fields only, 2 every field below 2^24 (default)
 void set_gemm_fold_f64(int mode) { g_gemm_fold_f64 = mode; }
+static int g_gemm_panel = -1;  // -1: the panel kernel where it pays, 0 never, 1 wherever Kp allows
+void set_gemm_panel(int mode) { g_gemm_panel = mode; }
 
 void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p, const int8_t* A,
                        const int8_t* B, int64_t b_plane, int value_bytes, void* C, int64_t ldc_z,
@@ -394,6 +510,34 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
   // second stage's r 2^28 + ... stays below 2^53 only for p < 2^24)
   const bool f64 = (g_gemm_fold_f64 == 2 && p < (1u << 24)) || (g_gemm_fold_f64 == 1 && limbs == 3);
   const int fold = f64 && fits53 ? 1 : (p >= (1u << 24) ? 2 : 0);
+  const int cnt_tiles = (N + kTileValues - 1) / kTileValues;
+  const int gx = (N + kBN - 1) / kBN, gy = (M + kBM - 1) / kBM;
+  // short K and enough row blocks to pay for loading the panel
+  if (Kp <= kPanelMaxK && (int64_t)gx * batches <= 0x7fffffff &&
+      (g_gemm_panel > 0 || (g_gemm_panel < 0 && gy >= 4))) {
+    dim3 grid((unsigned)(gx * batches));
+#define SDA_PANEL(VT, L, F)                                                                                  \
+  hipLaunchKernelGGL((k_modgemm_panel<VT, L, F>), grid, dim3(512), 0, s, M, N, Kp, batches, gx, gy, mp, mf, A, B, \
+                     b_plane, (VT*)C, ldc_z, ldc_m, ldc_n, limit, cnt, cnt_tiles)
+#define SDA_PANEL_VT(VT)                                                    \
+  do {                                                                      \
+    if (limbs == 3) {                                                       \
+      if (fold == 1) SDA_PANEL(VT, 3, 1); else SDA_PANEL(VT, 3, 0);         \
+    } else if (fold == 2) {                                                 \
+      SDA_PANEL(VT, 4, 2);                                                  \
+    } else if (fold == 1) {                                                 \
+      SDA_PANEL(VT, 4, 1);                                                  \
+    } else {                                                                \
+      SDA_PANEL(VT, 4, 0);                                                  \
+    }                                                                       \
+  } while (0)
+    if (value_bytes == 1) SDA_PANEL_VT(uint8_t);
+    else if (value_bytes == 2) SDA_PANEL_VT(uint16_t);
+    else SDA_PANEL_VT(uint32_t);
+#undef SDA_PANEL_VT
+#undef SDA_PANEL
+    return;
+  }
   GemmGrid gg;
   gg.gx = (N + kBN - 1) / kBN;
   gg.gy = (M + kBM - 1) / kBM;
@@ -411,7 +555,6 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
   const int64_t blocks = (int64_t)kXcds * gg.tiles_m * tiles_p * gg.gm * gg.gp;
   if (blocks > 0x7fffffff) return;  // cannot happen below 2^31 output tiles
   dim3 grid((unsigned)blocks);
-  const int cnt_tiles = (N + kTileValues - 1) / kTileValues;
 #define SDA_GEMM(VT, L, F)                                                                        \
   hipLaunchKernelGGL((k_modgemm_i8<VT, L, F>), grid, dim3(256), 0, s, M, N, Kp, batches, gg, mp, mf, A, B, b_plane, \
                      (VT*)C, ldc_z, ldc_m, ldc_n, limit, cnt, cnt_tiles)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Experiment: share GEMM of configs 6 / 8 alone, per epilogue fold (0 integer, 1 / 2 double-precision)."""
+"""Experiment: share GEMM of configs 6 / 8 alone, per kernel (general / panel-resident) and epilogue fold
+(0 integer, 2 double-precision)."""
 import os
 import sys
 
@@ -21,8 +22,9 @@ for c in (6, 8):
     out = torch.empty(n, P, B, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(n * P * G.tiles(B), dtype=torch.int32, device="cuda")
     ref = None
-    for mode in (0, 1, 2):
+    for panel, mode in ((0, 0), (0, 2), (1, 0), (1, 2)):
         gpu().set_gemm_fold_f64(mode)
+        gpu().set_gemm_panel(panel)
         for _ in range(2):
             cnt.zero_()
             G.modgemm_i8(A, X, p, out, ldc_z=B, ldc_m=P * B, ldc_n=1, limit=n * P * B, cnt=cnt)
@@ -35,7 +37,8 @@ for c in (6, 8):
         torch.cuda.synchronize()
         chk = int(out[::97, ::13, ::101].to(torch.int64).sum().item())
         ref = chk if ref is None else ref
-        print(f"config {c} fold mode {mode}: {e0.elapsed_time(e1) / 3:.2f} ms  checksum {'same' if chk == ref else 'DIFFERENT'}", flush=True)
-    gpu().set_gemm_fold_f64(2)  # the default
+        print(f"config {c} panel {panel} fold mode {mode}: {e0.elapsed_time(e1) / 3:.2f} ms  checksum {'same' if chk == ref else 'DIFFERENT'}", flush=True)
+    gpu().set_gemm_fold_f64(2)  # the defaults
+    gpu().set_gemm_panel(-1)
     del A, X, out, cnt
     torch.cuda.empty_cache()

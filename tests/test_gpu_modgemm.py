@@ -14,12 +14,15 @@ pytestmark = pytest.mark.gpu
                                           (433, 1), (433, 0), (16777213, 2), (16777213, 1),
                                           ((1 << 27) - 39, 2), ((1 << 27) - 39, 0),
                                           ((1 << 28) - 57, 2)])
-@pytest.mark.parametrize("M,N,K,Z", [(37, 45, 100, 2), (64, 64, 64, 1), (5, 300, 255, 3),
-                                     (130, 17, 700, 1)])
-def test_modgemm_matches_torch(cuda, prime, fold24, M, N, K, Z):
+@pytest.mark.parametrize("M,N,K,Z,panel", [(37, 45, 100, 2, 0), (64, 64, 64, 1, 0), (5, 300, 255, 3, 0),
+                                           (130, 17, 700, 1, 0), (37, 45, 100, 2, 1),
+                                           (5, 300, 255, 3, 1), (333, 200, 190, 2, 1),
+                                           (64, 128, 64, 1, 1)])
+def test_modgemm_matches_torch(cuda, prime, fold24, M, N, K, Z, panel):
     """Every epilogue: the 64-bit fold reduced through the double-precision unit (the
     default), and with it switched off the Horner chain of 32-bit Barrett steps
-    (p < 2^24) and the 64-bit Barrett fold (p >= 2^24)."""
+    (p < 2^24) and the 64-bit Barrett fold (p >= 2^24); under the general kernel and,
+    for K <= 256, the panel-resident one (one, two and six row blocks, ragged edges)."""
     from sda_amd._native import gpu
     from sda_amd.ops import gpu as G
 
@@ -32,11 +35,13 @@ def test_modgemm_matches_torch(cuda, prime, fold24, M, N, K, Z):
     Bl = torch.stack([G.limbs_of(Bm[z].to(torch.int32).cuda(), Kp, L) for z in range(Z)], 1)
     out = torch.zeros(Z * M * N, dtype=torch.int32, device="cuda")
     gpu().set_gemm_fold_f64(fold24)
+    gpu().set_gemm_panel(panel)
     try:
         G.modgemm_i8(Al.contiguous(), Bl.contiguous(), prime, out, ldc_z=M * N, ldc_m=N, ldc_n=1,
                      limit=Z * M * N)
     finally:
-        gpu().set_gemm_fold_f64(1)
+        gpu().set_gemm_fold_f64(2)
+        gpu().set_gemm_panel(-1)
     # exact reference: split K to keep int64 products exact
     ref = torch.stack([(A @ Bm[z].T) % prime for z in range(Z)]) if prime < 2 ** 21 else \
         torch.stack([sum((A[:, i:i + 1] * Bm[z][:, i:i + 1].T) % prime for i in range(K)) % prime
@@ -44,7 +49,9 @@ def test_modgemm_matches_torch(cuda, prime, fold24, M, N, K, Z):
     assert torch.equal(out.cpu().view(Z, M, N).to(torch.int64), ref)
 
 
-def test_modgemm_transposed_truncated_store(cuda):
+@pytest.mark.parametrize("panel", [0, 1])
+def test_modgemm_transposed_truncated_store(cuda, panel):
+    from sda_amd._native import gpu
     from sda_amd.ops import gpu as G
 
     p, k, R, N = 746497, 100, 255, 40
@@ -54,19 +61,26 @@ def test_modgemm_transposed_truncated_store(cuda):
     Kp = G.padded_k(R)
     D = k * N - 37  # truncation of the last batch
     out = torch.full((D,), -1, dtype=torch.int32, device="cuda")
-    G.modgemm_i8(G.limbs_of(Lm.to(torch.int32).cuda(), Kp, 3),
-                 G.limbs_t(Y.to(torch.int32).cuda(), Kp, 3), p, out, ldc_z=0, ldc_m=1, ldc_n=k,
-                 limit=D)
+    gpu().set_gemm_panel(panel)
+    try:
+        G.modgemm_i8(G.limbs_of(Lm.to(torch.int32).cuda(), Kp, 3),
+                     G.limbs_t(Y.to(torch.int32).cuda(), Kp, 3), p, out, ldc_z=0, ldc_m=1, ldc_n=k,
+                     limit=D)
+    finally:
+        gpu().set_gemm_panel(-1)
     ref = ((Lm @ Y) % p).T.reshape(-1)[:D]
     assert torch.equal(out.cpu().to(torch.int64), ref)
 
 
 @pytest.mark.parametrize("prime,dtype", [(746497, torch.int32), (5038849, torch.int32),
                                          (433, torch.int16), (60013, torch.int16)])
-@pytest.mark.parametrize("M,N,Z", [(37, 45, 2), (70, 4096 + 300, 3), (9, 9000, 1)])
-def test_modgemm_epilogue_counts_varint_bytes(cuda, prime, dtype, M, N, Z):
+@pytest.mark.parametrize("M,N,Z,panel", [(37, 45, 2, 0), (70, 4096 + 300, 3, 0), (9, 9000, 1, 0),
+                                         (37, 45, 2, 1), (270, 4096 + 300, 3, -1), (9, 9000, 1, 1)])
+def test_modgemm_epilogue_counts_varint_bytes(cuda, prime, dtype, M, N, Z, panel):
     """The share layout (C[m][z][n]) with `cnt`: the epilogue's byte counts per
-    (row, batch, 4096-column tile) equal the counting kernel's over the stored output."""
+    (row, batch, 4096-column tile) equal the counting kernel's over the stored output
+    (general kernel, panel-resident kernel, and the launcher's own choice)."""
+    from sda_amd._native import gpu
     from sda_amd.ops import gpu as G
 
     K = 130
@@ -81,8 +95,12 @@ def test_modgemm_epilogue_counts_varint_bytes(cuda, prime, dtype, M, N, Z):
     out = torch.zeros(M, Z, N, dtype=dtype, device="cuda")
     T = G.tiles(N)
     cnt = torch.zeros(M * Z * T, dtype=torch.int32, device="cuda")
-    G.modgemm_i8(Al.contiguous(), Bl.contiguous(), prime, out, ldc_z=N, ldc_m=Z * N, ldc_n=1,
-                 limit=M * Z * N, cnt=cnt)
+    gpu().set_gemm_panel(panel)
+    try:
+        G.modgemm_i8(Al.contiguous(), Bl.contiguous(), prime, out, ldc_z=N, ldc_m=Z * N, ldc_n=1,
+                     limit=M * Z * N, cnt=cnt)
+    finally:
+        gpu().set_gemm_panel(-1)
     ref = torch.empty(M * Z, T, dtype=torch.int32, device="cuda")
     G.count(out.view(M * Z, N), ref)
     assert torch.equal(cnt.view(M * Z, T), ref)
