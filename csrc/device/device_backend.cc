@@ -609,7 +609,7 @@ std::vector<int64_t> Backend::reveal(const Aggregation& agg, const EncryptionKey
       int8_t* X = mem.take<int8_t>((size_t)limbs * B * Kp);
       launch_limbs_t(nI, (int)B, Kp, limbs, ys, X, s_);
       launched("limbs_t");
-      launch_modgemm_i8((int)k, (int)B, Kp, 1, limbs, m, dA, X, (int64_t)B * Kp, 4, masked, 0, 1,
+      launch_modgemm_i8((int)k, (int)B, Kp, 1, limbs, m, dA, nullptr, X, (int64_t)B * Kp, 4, masked, 0, 1,
                         (int64_t)k, (int64_t)D, nullptr, s_);
       launched("modgemm_i8");
       sync();
@@ -786,13 +786,15 @@ DeviceParticipations Backend::participate_many(const Aggregation& agg,
           for (int j = 0; j < K; ++j)
             A[((size_t)l * n + c) * Kp + j] = (int8_t)((share_matrix[(size_t)c * K + j] >> (7 * l)) & 0x7f);
       int8_t* dA = to_device(mem, A);
+      int8_t* dAf = mem.take<int8_t>((size_t)a_fragments_bytes(n, Kp, limbs));
+      launch_a_fragments(n, Kp, limbs, dA, dAf, s_);
       int8_t* X = mem.take<int8_t>((size_t)limbs * P * B * Kp);
       launch_pss_x_limbs(P, (int)D, (int)B, (int)k, t_priv, Kp, limbs, m, masked, rng, 0, X, s_);
       launched("pss_x_limbs");
       // the boxes' varint bytes come out of the GEMM epilogue (cnt zeroed first; this
       // backend never runs inside a captured graph)
       HIP_OK(hipMemsetAsync(cnt, 0, (size_t)n * P * tiles(B) * sizeof(uint32_t), s_));
-      launch_modgemm_i8(n, (int)B, Kp, P, limbs, m, dA, X, (int64_t)P * B * Kp, value_bytes, shares,
+      launch_modgemm_i8(n, (int)B, Kp, P, limbs, m, dA, dAf, X, (int64_t)P * B * Kp, value_bytes, shares,
                         (int64_t)B, (int64_t)P * B, 1, (int64_t)n * P * B, cnt, s_);
       launched("modgemm_i8");
       sync();

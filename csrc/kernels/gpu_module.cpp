@@ -272,8 +272,14 @@ PYBIND11_MODULE(_sda_gpu, m) {
                            P<uint32_t>(out), S(stream));
     check_launch("pss_reconstruct");
   });
+  m.def("a_fragments_bytes", &a_fragments_bytes);
+  m.def("a_fragments", [](int M, int Kp, int limbs, uintptr_t A, uintptr_t out, uintptr_t stream) {
+    if (Kp % 64 != 0) throw std::invalid_argument("a_fragments: Kp must be a multiple of 64");
+    launch_a_fragments(M, Kp, limbs, P<const int8_t>(A), P<int8_t>(out), S(stream));
+    check_launch("a_fragments");
+  });
   m.def("modgemm_i8", [](int M, int N, int Kp, int batches, int limbs, uint32_t prime,
-                         uintptr_t A, uintptr_t B, int64_t b_plane, int value_bytes, uintptr_t C,
+                         uintptr_t A, uintptr_t a_frag, uintptr_t B, int64_t b_plane, int value_bytes, uintptr_t C,
                          int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit,
                          uintptr_t cnt, uintptr_t stream) {
     if (Kp % 64 != 0) throw std::invalid_argument("modgemm_i8: Kp must be a multiple of 64");
@@ -281,7 +287,7 @@ PYBIND11_MODULE(_sda_gpu, m) {
     if (prime >= (1u << (7 * limbs))) throw std::invalid_argument("modgemm_i8: modulus too large");
     if ((int64_t)Kp * 127 * 127 * limbs >= (int64_t)1 << 31)
       throw std::invalid_argument("modgemm_i8: K too large for int32 limb accumulators");
-    launch_modgemm_i8(M, N, Kp, batches, limbs, prime, P<const int8_t>(A), P<const int8_t>(B), b_plane,
+    launch_modgemm_i8(M, N, Kp, batches, limbs, prime, P<const int8_t>(A), P<const int8_t>(a_frag), P<const int8_t>(B), b_plane,
                       value_bytes, P<void>(C), ldc_z, ldc_m, ldc_n, limit, P<uint32_t>(cnt), S(stream));
     check_launch("modgemm_i8");
   });

@@ -546,6 +546,47 @@ int main() {
     CHECK(make_mod24(433, 7ull * 432 * 432).c != 0 && make_mod24(241, 5ull * 240 * 240).c != 0,
           "mod24 must cover the benchmark fields");
   }
+  // 7b. the double-precision reduction of the GEMM epilogue (quotient never too large,
+  //     at most one too small): multiples of m and their neighbours up to 2^53, random
+  //     values, for small, typical and the largest moduli; and the epilogue's varint
+  //     length formula against the threshold count
+  {
+    uint64_t x = 0x9e3779b97f4a7c15ull;
+    auto next = [&x] { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    for (uint32_t m : {16u, 17u, 433u, 60013u, 746497u, 5038849u, 16777213u, (1u << 27) - 39, (1u << 28) - 57}) {
+      const ModF64 P = make_modf64(m);
+      bool ok = true;
+      const uint64_t top = (1ull << 53) - 1;
+      for (int it = 0; it < 400000 && ok; ++it) {
+        const uint64_t r = next();
+        uint64_t v;
+        switch (it & 3) {
+          case 0: v = r & top; break;
+          case 1: v = ((r & top) / m) * m; break;                 // a multiple of m
+          case 2: v = ((r & top) / m) * m + (m - 1); break;       // just below one
+          default: v = top - (r % (4ull * m)); break;             // the top of the range
+        }
+        if (v > top) v = top;
+        ok = modf64d((double)v, P) == (uint32_t)(v % m);
+        if (!ok) std::printf("  v=%llu m=%u got %u\n", (unsigned long long)v, m, modf64d((double)v, P));
+      }
+      CHECK(ok, "modf64d m=%u", m);
+    }
+    bool ok = true;
+    for (uint64_t o = 0; o < (1ull << 29) && ok; o += (o < 70000 ? 1 : 997)) {
+      const uint32_t out = (uint32_t)o;
+      const uint32_t len = (1406u - 37u * (uint32_t)__builtin_clz((out << 1) | 1u)) >> 8;
+      const uint32_t ref = 1u + (out >= (1u << 6)) + (out >= (1u << 13)) + (out >= (1u << 20)) + (out >= (1u << 27));
+      ok = len == ref;
+    }
+    for (int b = 0; b < 29 && ok; ++b)
+      for (uint32_t out : {(1u << b) - 1, 1u << b, (1u << b) + 1}) {
+        const uint32_t len = (1406u - 37u * (uint32_t)__builtin_clz((out << 1) | 1u)) >> 8;
+        const uint32_t ref = 1u + (out >= (1u << 6)) + (out >= (1u << 13)) + (out >= (1u << 20)) + (out >= (1u << 27));
+        ok = ok && len == ref;
+      }
+    CHECK(ok, "varint length from the leading-zero count");
+  }
   // 8. the encode kernel's packed varint pairs against a plain zigzag-LEB128 encoder:
   //    every low value with a spread of high values, and the reverse
   {

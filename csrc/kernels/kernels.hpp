@@ -248,13 +248,21 @@ void launch_sub_mod(int D, uint32_t m, const uint32_t* a, const uint32_t* b, uin
 // cnt (may be null; zeroed by the caller): [M][batches][ceil(N / kTileValues)] varint
 // bytes of the written elements, i.e. launch_count's result for C as M x batches
 // messages of N values (the share GEMM: rows = clerks, batches = participants).
+// a_frag (may be null): A in the fragment order of launch_a_fragments; with it, short
+// K (Kp <= 256) and at least four row blocks the panel-resident kernel runs.
 void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p, const int8_t* A,
-                       const int8_t* B, int64_t b_plane, int value_bytes, void* C, int64_t ldc_z,
-                       int64_t ldc_m, int64_t ldc_n, int64_t limit, uint32_t* cnt, hipStream_t s);
+                       const int8_t* a_frag, const int8_t* B, int64_t b_plane, int value_bytes, void* C,
+                       int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit, uint32_t* cnt,
+                       hipStream_t s);
+// A limbs [L][M][Kp] reordered into `out` (a_fragments_bytes(M, Kp, limbs) bytes: M
+// rounded up to 64 rows): what each wave of the panel kernel loads is consecutive.
+int64_t a_fragments_bytes(int M, int Kp, int limbs);
+void launch_a_fragments(int M, int Kp, int limbs, const int8_t* A, int8_t* out, hipStream_t s);
 // epilogue fold through the double-precision unit: 0 never (integer only), 1 for
-// three-limb fields (default), 2 for four-limb fields too
+// three-limb fields only, 2 for every field below 2^24 (default)
 void set_gemm_fold_f64(int mode);
-// -1 (default): the panel-resident kernel for short K with at least four row blocks; 0 never; 1 whenever Kp <= 256
+// -1 (default): the panel-resident kernel for short K with at least four row blocks;
+// 0 never; 1 whenever Kp <= 256 (both need a_frag)
 void set_gemm_panel(int mode);
 // X limbs [3][P][B][Kp] of packed-Shamir inputs: secrets (canonical) then t draws.
 void launch_pss_x_limbs(int P, int D, int B, int k, int t, int Kp, int limbs, uint32_t p,

@@ -59,35 +59,26 @@ SDA_DEV uint32_t mod24(uint32_t w, const Mod24& P) {
   return w - (q & 0xffffffu) * (P.m & 0xffffffu);  // q, m < 2^24: a 24-bit multiply-subtract
 }
 // Exact reduction of an integer 0 <= v < 2^53 through the double-precision unit (full
-// rate on this chip, like the 32-bit integer multiplies): q = trunc(v * (1/m)) is
-// floor(v / m) or off by one (v / m < 2^33 and the two roundings move it by less than
-// 2^-18), v - q m is then exact in one fused multiply-add, and two corrections bring
-// it into [0, m). Eleven instructions, whatever v's size -- a 64-bit Barrett step
-// (mod64) takes about thirty.
+// rate on this chip, like the 32-bit integer multiplies), for m >= 16. `inv` is 1/m
+// scaled down by 2^-50: with the three roundings on the way (1/m, the scaling, the
+// product; 2^-53 each) v * inv lies in (v/m (1 - 11 2^-53), v/m), so q = trunc(v * inv)
+// is floor(v / m) or one less (v/m 11 2^-53 < 1), never more; v - q m, exact in one
+// fused multiply-add, is in [0, 2m) and one conditional subtraction finishes. Seven
+// instructions, whatever v's size -- a 64-bit Barrett step (mod64) takes about thirty.
 struct ModF64 {
   double m, inv;
 };
-inline ModF64 make_modf64(uint32_t m) { return ModF64{(double)m, m ? 1.0 / (double)m : 0.0}; }
+inline ModF64 make_modf64(uint32_t m) {
+  return ModF64{(double)m, m ? (1.0 / (double)m) * (1.0 - 0x1p-50) : 0.0};
+}
 // v given as a double (an exact integer below 2^53)
 SDA_DEV uint32_t modf64d(double vd, const ModF64& P) {
   const double q = __builtin_trunc(vd * P.inv);
-  int32_t r = (int32_t)__builtin_fma(-q, P.m, vd);  // in (-m, 2m)
-  const int32_t m = (int32_t)P.m;
-  r += (r >> 31) & m;
-  r -= m;
-  r += (r >> 31) & m;
-  return (uint32_t)r;
+  const uint32_t r = (uint32_t)__builtin_fma(-q, P.m, vd);  // in [0, 2m)
+  const uint32_t t = r - (uint32_t)P.m;                     // wraps above r when r < m
+  return t < r ? t : r;
 }
-SDA_DEV uint32_t modf64(uint64_t v, const ModF64& P) {
-  const double vd = (double)(int64_t)v;
-  const double q = __builtin_trunc(vd * P.inv);
-  int32_t r = (int32_t)__builtin_fma(-q, P.m, vd);  // in (-m, 2m)
-  const int32_t m = (int32_t)P.m;
-  r += (r >> 31) & m;
-  r -= m;
-  r += (r >> 31) & m;
-  return (uint32_t)r;
-}
+SDA_DEV uint32_t modf64(uint64_t v, const ModF64& P) { return modf64d((double)(int64_t)v, P); }
 SDA_DEV uint32_t mod64(uint64_t v, const ModParams& P) {
   uint64_t q = __umul64hi(v, P.mu64);
   uint64_t r = v - q * (uint64_t)P.m;  // q >= floor(v/m) - 2

@@ -69,86 +69,110 @@ SDA_DEV int swz(int row, int chunk) {  // position of a row's 16-byte chunk insi
 // Epilogue of a wave's 32 x 16 kJT outputs held as degree sums in `acc` (rows from
 // m_blk + 32 wm, columns from n_blk + 16 kJT wn, C/D map of the 16x16 MFMA): fold,
 // store, and -- with `cnt` -- the byte counts.
-template <typename VT, int kLimbs, int kFold, int kJT>
+template <typename VT, int kLimbs, int kFold, int kJT, bool kVec>
 __device__ __forceinline__ void gemm_epilogue(const v4i (&acc)[2][kJT][2 * kLimbs - 1], int m_blk, int n_blk,
                                               int z, int wm, int wn, int lane, int M, int N, int batches,
                                               const ModParams& mp, const ModF64& mf, VT* __restrict__ C,
                                               int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit,
                                               uint32_t* __restrict__ cnt, int cnt_tiles) {
   constexpr int kDeg = 2 * kLimbs - 1;
-  // epilogue: C/D map col = lane & 15, row = 4*(lane >> 4) + r. Output indices are
-  // built from per-lane bases by additions (the general z/m/n strides would cost
-  // three 64-bit multiplies per element otherwise).
+  // C/D map of the MFMA: tile column lane & 15, tile row 4*(lane >> 4) + r. Which matrix
+  // column a tile column stands for is the caller's choice of B rows: tile j's column c
+  // is column 16 j + c of the wave's 16 kJT, or -- kVec -- column kJT c + j: a lane's
+  // kJT outputs of one row are then neighbours in memory and leave in one store.
+  // Output indices are built from per-lane bases by additions (the general z/m/n strides
+  // would cost three 64-bit multiplies per element otherwise).
   uint32_t w[kDeg];
   if constexpr (kFold == 2) {
 #pragma unroll
     for (int d = 0; d < kDeg; ++d) w[d] = (uint32_t)(((uint64_t)1 << (kLimbBits * d)) % mp.m);
   }
   const int row0 = m_blk + wm * 32 + 4 * (lane >> 4);
-  const int col0 = n_blk + wn * (16 * kJT) + (lane & 15);
+  const int col0 = n_blk + wn * (16 * kJT) + (kVec ? kJT : 1) * (lane & 15);
+  constexpr int kColStep = kVec ? 1 : 16;  // matrix columns between tiles j and j + 1
   const int64_t base = (int64_t)z * ldc_z + (int64_t)row0 * ldc_m + (int64_t)col0 * ldc_n;
-  const int64_t step_j = 16 * ldc_n, step_i = 16 * ldc_m;
+  const int64_t step_j = kColStep * ldc_n, step_i = 16 * ldc_m;
   uint32_t bytes[2][2] = {{0, 0}, {0, 0}};  // varint bytes of rows (i, r): two 16-bit sums per word
+  auto fold = [&](int i, int j, int r) -> uint32_t {
+    if constexpr (kFold == 1) {
+      // neighbouring degrees pair up in 32 bits (acc_d 2^7 + acc_(d-1) < 2^32: the
+      // caller's bound on K), the pairs meet as doubles: exact integers below 2^53
+      auto pair = [&](int d) -> double {  // acc_(d+1) 2^7 + acc_d, or acc_d alone at the top
+        uint32_t v = (uint32_t)acc[i][j][d][r];
+        if (d + 1 < kDeg) v += (uint32_t)acc[i][j][d + 1][r] << kLimbBits;
+        return (double)v;
+      };
+      if constexpr (kLimbs == 3) {
+        const double s = __builtin_fma(pair(4), 268435456.0, __builtin_fma(pair(2), 16384.0, pair(0)));
+        return modf64d(s, mf);
+      } else {
+        // degrees 4..6 first (below 2^46), reduced; then with the low four (below 2^53)
+        const double hi = __builtin_fma(pair(6), 16384.0, pair(4));
+        const double rh = (double)modf64d(hi, mf);
+        const double s = __builtin_fma(rh, 268435456.0, __builtin_fma(pair(2), 16384.0, pair(0)));
+        return modf64d(s, mf);
+      }
+    } else if constexpr (kFold == 0) {
+      // acc_d < 2^31, s < p < 2^24: s * 2^7 + acc_d < 2^32
+      uint32_t s = mod32((uint32_t)acc[i][j][kDeg - 1][r], mp);
+#pragma unroll
+      for (int d = kDeg - 2; d >= 0; --d) s = mod32((s << kLimbBits) + (uint32_t)acc[i][j][d][r], mp);
+      return s;
+    } else {
+      uint64_t s = 0;
+#pragma unroll
+      for (int d = 0; d < kDeg; ++d)
+        s += (uint64_t)mod32((uint32_t)acc[i][j][d][r], mp) * w[d];  // < 7 * 2^56
+      return mod64(s, mp);
+    }
+  };
+  // zigzag code z = 2 * out of b bits (b of 2 * out + 1: the same, and 1 for 0):
+  // ceil(b / 7) bytes = ((b + 6) * 37) >> 8 for b + 6 <= 35, b = 32 - clz
+  auto varint_len = [](uint32_t out) -> uint32_t {
+    return (1406u - 37u * (uint32_t)__builtin_clz((out << 1) | 1u)) >> 8;
+  };
   // A block whose whole tile is inside the matrix and below `limit` (nine in ten of the
   // share GEMMs' blocks) stores without any per-element test: the tests are a compare
   // or two and a branch per element otherwise.
-  const bool inside = m_blk + kBM <= M && n_blk + kBN <= N && limit < 0;  // block-uniform
-  auto tile_out = [&](auto interior) {
-    constexpr bool kInterior = decltype(interior)::value;
+  const bool inside = m_blk + kBM <= M && n_blk + kBN <= N && limit < 0 && (!kVec || ldc_n == 1);  // uniform
+  if (inside) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = row0 + 16 * i + r;
-      if (!kInterior && row >= M) continue;
-      int64_t idx = base + i * step_i + r * ldc_m;
+      for (int r = 0; r < 4; ++r) {
+        const int64_t idx = base + i * step_i + r * ldc_m;
+        VT o[kJT];
 #pragma unroll
-      for (int j = 0; j < kJT; ++j, idx += step_j) {
-        if (!kInterior && col0 + 16 * j >= N) continue;
-        uint32_t out;
-        if constexpr (kFold == 1) {
-          // neighbouring degrees pair up in 32 bits (acc_d 2^7 + acc_(d-1) < 2^32: the
-          // caller's bound on K), the pairs meet as doubles: exact integers below 2^53
-          auto pair = [&](int d) -> double {  // acc_(d+1) 2^7 + acc_d, or acc_d alone at the top
-            uint32_t v = (uint32_t)acc[i][j][d][r];
-            if (d + 1 < kDeg) v += (uint32_t)acc[i][j][d + 1][r] << kLimbBits;
-            return (double)v;
-          };
-          if constexpr (kLimbs == 3) {
-            const double s = __builtin_fma(pair(4), 268435456.0, __builtin_fma(pair(2), 16384.0, pair(0)));
-            out = modf64d(s, mf);
-          } else {
-            // degrees 4..6 first (below 2^46), reduced; then with the low four (below 2^53)
-            const double hi = __builtin_fma(pair(6), 16384.0, pair(4));
-            const double rh = (double)modf64d(hi, mf);
-            const double s = __builtin_fma(rh, 268435456.0, __builtin_fma(pair(2), 16384.0, pair(0)));
-            out = modf64d(s, mf);
-          }
-        } else if constexpr (kFold == 0) {
-          // acc_d < 2^31, s < p < 2^24: s * 2^7 + acc_d < 2^32
-          uint32_t s = mod32((uint32_t)acc[i][j][kDeg - 1][r], mp);
-#pragma unroll
-          for (int d = kDeg - 2; d >= 0; --d) s = mod32((s << kLimbBits) + (uint32_t)acc[i][j][d][r], mp);
-          out = s;
-        } else {
-          uint64_t s = 0;
-#pragma unroll
-          for (int d = 0; d < kDeg; ++d)
-            s += (uint64_t)mod32((uint32_t)acc[i][j][d][r], mp) * w[d];  // < 7 * 2^56
-          out = mod64(s, mp);
+        for (int j = 0; j < kJT; ++j) {
+          const uint32_t out = fold(i, j, r);
+          o[j] = (VT)out;
+          bytes[i][r >> 1] += varint_len(out) << (16 * (r & 1));
         }
-        if (kInterior || limit < 0 || idx < limit) {  // limit < 0: every in-range element is stored
-          C[idx] = (VT)out;
-          // zigzag code 2 * out: one byte below 2^6, two below 2^13, ...
-          uint32_t len = 1u + (out >= (1u << 6)) + (out >= (1u << 13)) + (out >= (1u << 20));
-          if constexpr (kLimbs > 3) len += out >= (1u << 27);
-          bytes[i][r >> 1] += len << (16 * (r & 1));
+        if constexpr (kVec) {
+          __builtin_memcpy(C + idx, o, sizeof(o));  // one store of kJT neighbours (C is only VT-aligned)
+        } else {
+#pragma unroll
+          for (int j = 0; j < kJT; ++j) C[idx + j * step_j] = o[j];
         }
       }
-    }
-  };
-  if (inside) tile_out(std::true_type{});
-  else tile_out(std::false_type{});
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + 16 * i + r;
+        if (row >= M) continue;
+        int64_t idx = base + i * step_i + r * ldc_m;
+#pragma unroll
+        for (int j = 0; j < kJT; ++j, idx += step_j) {
+          if (col0 + kColStep * j >= N) continue;
+          if (limit >= 0 && idx >= limit) continue;  // limit < 0: every in-range element is stored
+          const uint32_t out = fold(i, j, r);
+          C[idx] = (VT)out;
+          bytes[i][r >> 1] += varint_len(out) << (16 * (r & 1));
+        }
+      }
+  }
   if (cnt == nullptr) return;  // uniform
   // the block's 128 columns lie inside one count tile (kTileValues is a multiple of kBN)
   static_assert(kTileValues % kBN == 0, "a block's columns must not straddle a count tile");
@@ -288,8 +312,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     if (ks + 1 < nk) commit(cur ^ 1);
     __syncthreads();
   }
-  gemm_epilogue<VT, kLimbs, kFold, 4>(acc, m_blk, n_blk, z, wm, wn, lane, M, N, batches, mp, mf, C, ldc_z,
-                                      ldc_m, ldc_n, limit, cnt, cnt_tiles);
+  gemm_epilogue<VT, kLimbs, kFold, 4, false>(acc, m_blk, n_blk, z, wm, wn, lane, M, N, batches, mp, mf, C, ldc_z,
+                                             ldc_m, ldc_n, limit, cnt, cnt_tiles);
 }
 
 // The same product for short K (Kp <= 256: share generation, K = t + k), one workgroup
@@ -300,11 +324,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 // panel's limbs (128 columns x Kp x L bytes, 96 / 128 KB) are loaded into LDS once and
 // the workgroup walks down all row blocks of A against them. A is small and shared by
 // every panel (it stays in each XCD's L2), so each wave loads its own A fragments
-// straight from global memory in the MFMA operand layout -- lane (r, g) takes bytes
-// [16 g, 16 g + 16) of row r of the K-step -- one step ahead of the MFMAs that use
-// them. After the panel is in LDS nothing is written to it and no wave waits for
-// another: the two waves of a SIMD drift apart, and one's epilogue fills the issue
-// slots under the other's MFMAs.
+// straight from global memory, one step ahead of the MFMAs that use them, from a copy of
+// A in fragment order (launch_a_fragments: [row block][K-step][limb][16-row tile][lane]
+// [16 bytes], lane (r, g) = bytes [16 g, 16 g + 16) of row r): one load instruction is
+// 1 KB of consecutive bytes. (From the row-major limbs the same instruction touched 16
+// half cache lines; the A traffic alone then held the kernel at 11.6 ms of 19.) After
+// the panel is in LDS nothing is written to it and no wave waits for another.
+// The panel's rows are stored so that MFMA tile j's column c is column kJT c + j of the
+// wave's columns: a lane's kJT outputs of a row are neighbours in C and leave in one
+// 16-byte store (the plain order gives 4-byte stores, 64 B runs per instruction; the
+// stores cost 5.5 of the 19 ms).
 // Eight waves: with three limbs two teams of 2 x 2 waves (32 x 64 outputs per wave, 120
 // accumulator registers) take alternate row blocks; with four limbs one team of 2 x 4
 // (32 x 32 per wave, 112 registers).
@@ -313,7 +342,7 @@ constexpr int kPanelMaxK = 256;
 template <typename VT, int kLimbs, int kFold>
 __global__ void __launch_bounds__(512)
     k_modgemm_panel(int M, int N, int Kp, int batches, int gx, int gy, ModParams mp, ModF64 mf,
-                    const int8_t* __restrict__ A, const int8_t* __restrict__ B, int64_t b_batch,
+                    const int8_t* __restrict__ Afrag, const int8_t* __restrict__ B, int64_t b_batch,
                     VT* __restrict__ C, int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit,
                     uint32_t* __restrict__ cnt, int cnt_tiles) {
   constexpr int kDeg = 2 * kLimbs - 1;
@@ -340,7 +369,9 @@ __global__ void __launch_bounds__(512)
     for (int u = 0; u < kMine; ++u) {
       const int id = u * 512 + tid;
       const int c = id % cpr, rl = id / cpr, row = rl % kBN, l = rl / kBN;
-      const int grow = n_blk + row;
+      // LDS row `row` = tile (row / 16) % kJT, tile column row % 16 of wave row / (16 kJT)
+      constexpr int kW = 16 * kJT;
+      const int grow = n_blk + (row / kW) * kW + kJT * (row & 15) + ((row >> 4) % kJT);
       const bool ok = id < pieces;
       dst[u] = ok ? ((l * kSteps + (c >> 2)) * kBN + row) * kBK + 16 * swz(row, c & 3) : -1;
       t[u] = ok && grow < N ? *reinterpret_cast<const v4i*>(Bz + l * b_batch + (int64_t)grow * Kp + 16 * c)
@@ -351,34 +382,47 @@ __global__ void __launch_bounds__(512)
       if (dst[u] >= 0) *reinterpret_cast<v4i*>(Bs + dst[u]) = t[u];
   }
   __syncthreads();
+  // Waves 0-3 and 4-7 share the four SIMDs pairwise and do identical work: left alone
+  // they stay in step -- both in their MFMAs, then both in their epilogues, each at half
+  // speed, nothing overlapped. Holding the second four back by about one tile's MFMAs
+  // (4,096 cycles) once puts one wave's epilogue under the other's MFMAs from then on.
+  if (wave >= 4) __builtin_amdgcn_s_sleep(64);
 
   const int fr = lane & 15, fg = lane >> 4;
   const int b_off = (wn * (16 * kJT) + fr) * kBK + 16 * swz(fr, fg);
-  const int64_t a_plane = (int64_t)M * Kp;
-  // rows past M read row M - 1: their outputs are never stored
+  // this wave's two 16-row tiles of (row block mb, step ks), limb l: 1 KB each
+  const int8_t* af = Afrag + ((int64_t)(2 * wm) * 64 + lane) * 16;
   auto load_a = [&](v4i (&f)[2][kLimbs], int mb, int ks) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = min(mb * kBM + wm * 32 + 16 * i + fr, M - 1);
-      const int8_t* p = A + (int64_t)row * Kp + ks * kBK + 16 * fg;
-#pragma unroll
-      for (int l = 0; l < kLimbs; ++l) f[i][l] = *reinterpret_cast<const v4i*>(p + l * a_plane);
-    }
-  };
-  v4i fa[2][kLimbs], fnext[2][kLimbs];
-  if (team < gy) load_a(fa, team, 0);
-  for (int mb = team; mb < gy; mb += kTeams) {
-    v4i acc[2][kJT][kDeg];
+    const int8_t* p = af + (int64_t)(mb * nk + ks) * (kLimbs * 4096);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < kJT; ++j)
+      for (int l = 0; l < kLimbs; ++l) f[i][l] = *reinterpret_cast<const v4i*>(p + (l * 4 + i) * 1024);
+  };
+  // The next step's fragments are requested before this step's MFMAs and taken over
+  // after them -- a K-step of MFMAs (1,152 cycles) covers the L2 latency. The loads are
+  // unconditional (past the last row block they fetch row block `mb` again) and the
+  // hand-over sits before the epilogue: with a branch around the loads, or the
+  // epilogue's stores between request and use, the compiler's wait-count bookkeeping
+  // turns conservative and every step waits for the loads it has just issued.
+  v4i fa[2][kLimbs], fnext[2][kLimbs];
+  auto take = [&] {
 #pragma unroll
-        for (int d = 0; d < kDeg; ++d) acc[i][j][d] = v4i{0, 0, 0, 0};
-    for (int ks = 0; ks < nk; ++ks) {
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int l = 0; l < kLimbs; ++l) fa[i][l] = fnext[i][l];
+  };
+  load_a(fnext, min(team, gy - 1), 0);
+  take();
+  for (int mb = team; mb < gy; mb += kTeams) {
+    v4i acc[2][kJT][kDeg];
+    // the first K-step starts every degree from a zero C operand: no clearing pass
+    auto step = [&](int ks, auto first) {
+      constexpr bool kFirst = decltype(first)::value;
       const bool more = ks + 1 < nk;
-      const int nmb = more ? mb : mb + kTeams;
-      if (nmb < gy) load_a(fnext, nmb, more ? ks + 1 : 0);
+      const int nmb = more || mb + kTeams >= gy ? mb : mb + kTeams;
+      load_a(fnext, nmb, more ? ks + 1 : 0);
+      __builtin_amdgcn_sched_barrier(0);  // or the scheduler sinks the loads below the MFMAs
       const int8_t* base = Bs + ks * kPlane + b_off;
 #pragma unroll
       for (int j = 0; j < kJT; ++j) {
@@ -391,16 +435,20 @@ __global__ void __launch_bounds__(512)
 #pragma unroll
           for (int la = 0; la < kLimbs; ++la)
 #pragma unroll
-            for (int lb = 0; lb < kLimbs; ++lb)
-              acc[i][j][la + lb] =
-                  __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i][la], fb[lb], acc[i][j][la + lb], 0, 0, 0);
+            for (int lb = 0; lb < kLimbs; ++lb) {
+              // (la, lb) with la == 0 or lb == kLimbs - 1 is its degree's first product
+              const bool fresh = kFirst && (la == 0 || lb == kLimbs - 1);
+              acc[i][j][la + lb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                  fa[i][la], fb[lb], fresh ? v4i{0, 0, 0, 0} : acc[i][j][la + lb], 0, 0, 0);
+            }
       }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int l = 0; l < kLimbs; ++l) fa[i][l] = fnext[i][l];
-    }
-    gemm_epilogue<VT, kLimbs, kFold, kJT>(acc, mb * kBM, n_blk, z, wm, wn, lane, M, N, batches, mp, mf, C,
+      __builtin_amdgcn_sched_barrier(0);
+      take();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    step(0, std::true_type{});
+    for (int ks = 1; ks < nk; ++ks) step(ks, std::false_type{});
+    gemm_epilogue<VT, kLimbs, kFold, kJT, true>(acc, mb * kBM, n_blk, z, wm, wn, lane, M, N, batches, mp, mf, C,
                                           ldc_z, ldc_m, ldc_n, limit, cnt, cnt_tiles);
   }
 }
@@ -483,7 +531,33 @@ __global__ void __launch_bounds__(256)
   put_limbs<kLimbs>(out + (int64_t)col * Kp + 16 * g, (int64_t)N * Kp, v);
 }
 
+// A limbs [L][M][Kp] in the order the panel kernel's waves load them: [row block]
+// [K-step][limb][16-row tile (4)][lane (64)][16 bytes], lane (r, g) holding bytes
+// [16 g, 16 g + 16) of the step of row r of the tile; rows past M are zero.
+__global__ void __launch_bounds__(256)
+    k_a_fragments(int M, int Kp, int limbs, const int8_t* __restrict__ A, int8_t* __restrict__ out) {
+  const int nk = Kp / kBK, gy = (M + kBM - 1) / kBM;
+  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (int64_t)gy * nk * limbs * 256) return;
+  const int lane = (int)(id & 63), t = (int)((id >> 6) & 3);
+  const int64_t rest = id >> 8;
+  const int l = (int)(rest % limbs), ks = (int)((rest / limbs) % nk), mb = (int)(rest / limbs / nk);
+  const int row = mb * kBM + 16 * t + (lane & 15), col = ks * kBK + 16 * (lane >> 4);
+  v4i v = {0, 0, 0, 0};
+  if (row < M) v = *reinterpret_cast<const v4i*>(A + ((int64_t)l * M + row) * Kp + col);
+  *reinterpret_cast<v4i*>(out + id * 16) = v;
+}
+
 }  // namespace
+
+int64_t a_fragments_bytes(int M, int Kp, int limbs) {
+  return (int64_t)((M + kBM - 1) / kBM) * kBM * Kp * limbs;
+}
+void launch_a_fragments(int M, int Kp, int limbs, const int8_t* A, int8_t* out, hipStream_t s) {
+  if (M <= 0) return;
+  const int64_t pieces = a_fragments_bytes(M, Kp, limbs) / 16;
+  hipLaunchKernelGGL(k_a_fragments, dim3((unsigned)((pieces + 255) / 256)), dim3(256), 0, s, M, Kp, limbs, A, out);
+}
 
 static int g_gemm_fold_f64 = 2;  // 0 never, 1 three-limb fields only, 2 every field below 2^24 (default)
 void set_gemm_fold_f64(int mode) { g_gemm_fold_f64 = mode; }
@@ -491,8 +565,9 @@ static int g_gemm_panel = -1;  // -1: the panel kernel where it pays, 0 never, 1
 void set_gemm_panel(int mode) { g_gemm_panel = mode; }
 
 void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p, const int8_t* A,
-                       const int8_t* B, int64_t b_plane, int value_bytes, void* C, int64_t ldc_z,
-                       int64_t ldc_m, int64_t ldc_n, int64_t limit, uint32_t* cnt, hipStream_t s) {
+                       const int8_t* a_frag, const int8_t* B, int64_t b_plane, int value_bytes, void* C,
+                       int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit, uint32_t* cnt,
+                       hipStream_t s) {
   if (M <= 0 || N <= 0 || batches <= 0) return;
   ModParams mp = make_mod_params(p);
   const ModF64 mf = make_modf64(p);
@@ -508,16 +583,16 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
   // measured on the share GEMMs of the two large reference fields, against the Horner
   // chain: three limbs 28.9 -> 27.8 ms, four limbs 21.0 -> 20.4 ms (four limbs: the
   // second stage's r 2^28 + ... stays below 2^53 only for p < 2^24)
-  const bool f64 = (g_gemm_fold_f64 == 2 && p < (1u << 24)) || (g_gemm_fold_f64 == 1 && limbs == 3);
+  const bool f64 = p >= 16 && ((g_gemm_fold_f64 == 2 && p < (1u << 24)) || (g_gemm_fold_f64 == 1 && limbs == 3));
   const int fold = f64 && fits53 ? 1 : (p >= (1u << 24) ? 2 : 0);
   const int cnt_tiles = (N + kTileValues - 1) / kTileValues;
   const int gx = (N + kBN - 1) / kBN, gy = (M + kBM - 1) / kBM;
   // short K and enough row blocks to pay for loading the panel
-  if (Kp <= kPanelMaxK && (int64_t)gx * batches <= 0x7fffffff &&
+  if (a_frag != nullptr && Kp <= kPanelMaxK && (int64_t)gx * batches <= 0x7fffffff &&
       (g_gemm_panel > 0 || (g_gemm_panel < 0 && gy >= 4))) {
     dim3 grid((unsigned)(gx * batches));
 #define SDA_PANEL(VT, L, F)                                                                                  \
-  hipLaunchKernelGGL((k_modgemm_panel<VT, L, F>), grid, dim3(512), 0, s, M, N, Kp, batches, gx, gy, mp, mf, A, B, \
+  hipLaunchKernelGGL((k_modgemm_panel<VT, L, F>), grid, dim3(512), 0, s, M, N, Kp, batches, gx, gy, mp, mf, a_frag, B, \
                      b_plane, (VT*)C, ldc_z, ldc_m, ldc_n, limit, cnt, cnt_tiles)
 #define SDA_PANEL_VT(VT)                                                    \
   do {                                                                      \

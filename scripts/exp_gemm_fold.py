@@ -11,7 +11,14 @@ from sda_amd._native import gpu  # noqa: E402
 from sda_amd.models.configs import bench_config  # noqa: E402
 from sda_amd.ops import gpu as G  # noqa: E402
 
-for c in (6, 8):
+# usage: exp_gemm_fold.py [config ...] [--only PANEL:FOLD]
+args = sys.argv[1:]
+only = None
+if "--only" in args:
+    i = args.index("--only")
+    only = tuple(int(v) for v in args[i + 1].split(":"))
+    del args[i:i + 2]
+for c in [int(a) for a in args] or (6, 8):
     cfg = bench_config(c)
     ps = cfg.sharing()
     p, n, K = ps.field_modulus, ps.share_count, ps.secret_count + ps.privacy_threshold_
@@ -22,7 +29,7 @@ for c in (6, 8):
     out = torch.empty(n, P, B, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(n * P * G.tiles(B), dtype=torch.int32, device="cuda")
     ref = None
-    for panel, mode in ((0, 0), (0, 2), (1, 0), (1, 2)):
+    for panel, mode in ((only,) if only else ((0, 0), (0, 2), (1, 0), (1, 2))):
         gpu().set_gemm_fold_f64(mode)
         gpu().set_gemm_panel(panel)
         for _ in range(2):

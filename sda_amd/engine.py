@@ -181,6 +181,7 @@ class DeviceAggregator:
                 self._M_limbs = G.limbs_of(
                     self._share_matrix.view(self.n, ps.secret_count + ps.privacy_threshold_),
                     self._Kp, self._limbs)
+                self._M_frag = G.a_fragments(self._M_limbs) if self._Kp <= G.PANEL_MAX_K else None
         else:
             self._pss = None
             self._pss_mfma = False
@@ -231,7 +232,7 @@ class DeviceAggregator:
             X = G.pss_x_limbs(masked, ps.secret_count, ps.privacy_threshold_, m, rng_key, owner_base)
             cnt.zero_()  # the GEMM epilogue adds the boxes' varint bytes into it
             G.modgemm_i8(self._M_limbs, X, m, shares, ldc_z=B, ldc_m=P * B, ldc_n=1,
-                         limit=n * P * B, cnt=cnt)
+                         limit=n * P * B, cnt=cnt, a_frag=self._M_frag)
             return shares, cnt, mask_vals, mask_cnt
         mode = G.MASK_FULL if full else G.MASK_NONE
         if self._pss is None:

@@ -510,9 +510,26 @@ def limbs_of(values: torch.Tensor, Kp: int, limbs: int) -> torch.Tensor:
     return out
 
 
+PANEL_MAX_K = 256  # the panel-resident GEMM kernel's longest (padded) K
+
+
+def a_fragments(A_limbs: torch.Tensor) -> torch.Tensor:
+    """A limbs [L][M][Kp] in the order the panel-resident GEMM kernel's waves load them
+    (rows padded to a multiple of 64): pass as `a_frag` to :func:`modgemm_i8`."""
+    _check(A_limbs, "A_limbs", torch.int8)
+    L, M, Kp = A_limbs.shape
+    out = torch.empty(_gpu().a_fragments_bytes(M, Kp, L), dtype=torch.int8, device=A_limbs.device)
+    _gpu().a_fragments(M, Kp, L, _ptr(A_limbs), _ptr(out), _stream())
+    return out
+
+
 def modgemm_i8(A_limbs: torch.Tensor, B_limbs: torch.Tensor, prime: int, out: torch.Tensor,
-               ldc_z: int, ldc_m: int, ldc_n: int, limit: int, cnt: torch.Tensor | None = None):
+               ldc_z: int, ldc_m: int, ldc_n: int, limit: int, cnt: torch.Tensor | None = None,
+               a_frag: torch.Tensor | None = None):
     """out[z*ldc_z + m*ldc_m + n*ldc_n] = (A . B_z)[m][n] mod prime (A [L][M][Kp], B [L][Z][N][Kp]).
+
+    `a_frag`: :func:`a_fragments` of A_limbs (made here when K is short and it is not
+    given -- a caller that reuses A keeps it): the panel-resident kernel needs it.
 
     `cnt` (int32 [M * Z * tiles(N)], zeroed): the epilogue also adds up the varint
     bytes of what it writes, per (row m, batch z, 4096-column tile) -- :func:`count`
@@ -533,7 +550,14 @@ def modgemm_i8(A_limbs: torch.Tensor, B_limbs: torch.Tensor, prime: int, out: to
         _check(cnt, "cnt", torch.int32)
         if cnt.numel() < M * Z * tiles(N):
             raise ValueError("cnt too small")
-    _gpu().modgemm_i8(M, N, Kp, Z, L, prime, _ptr(A_limbs), _ptr(B_limbs), Z * N * Kp, vb,
+    if a_frag is None and Kp <= PANEL_MAX_K:
+        a_frag = a_fragments(A_limbs)
+    if a_frag is not None:
+        _check(a_frag, "a_frag", torch.int8)
+        if a_frag.numel() != _gpu().a_fragments_bytes(M, Kp, L):
+            raise ValueError("a_frag does not belong to A_limbs")
+    _gpu().modgemm_i8(M, N, Kp, Z, L, prime, _ptr(A_limbs), 0 if a_frag is None else _ptr(a_frag),
+                      _ptr(B_limbs), Z * N * Kp, vb,
                       _ptr(out), ldc_z, ldc_m, ldc_n, limit, 0 if cnt is None else _ptr(cnt),
                       _stream())
 

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
                                           ((1 << 28) - 57, 2)])
 @pytest.mark.parametrize("M,N,K,Z,panel", [(37, 45, 100, 2, 0), (64, 64, 64, 1, 0), (5, 300, 255, 3, 0),
                                            (130, 17, 700, 1, 0), (37, 45, 100, 2, 1),
-                                           (5, 300, 255, 3, 1), (333, 200, 190, 2, 1),
+                                           (5, 300, 255, 3, 1), (333, 200, 190, 2, 1), (130, 301, 100, 2, 1),
                                            (64, 128, 64, 1, 1)])
 def test_modgemm_matches_torch(cuda, prime, fold24, M, N, K, Z, panel):
     """Every epilogue: the 64-bit fold reduced through the double-precision unit (the
@@ -75,7 +75,8 @@ def test_modgemm_transposed_truncated_store(cuda, panel):
 @pytest.mark.parametrize("prime,dtype", [(746497, torch.int32), (5038849, torch.int32),
                                          (433, torch.int16), (60013, torch.int16)])
 @pytest.mark.parametrize("M,N,Z,panel", [(37, 45, 2, 0), (70, 4096 + 300, 3, 0), (9, 9000, 1, 0),
-                                         (37, 45, 2, 1), (270, 4096 + 300, 3, -1), (9, 9000, 1, 1)])
+                                         (37, 45, 2, 1), (270, 4096 + 300, 3, -1), (9, 9000, 1, 1),
+                                         (130, 4097 + 300, 2, 1)])  # odd N: unaligned wide stores
 def test_modgemm_epilogue_counts_varint_bytes(cuda, prime, dtype, M, N, Z, panel):
     """The share layout (C[m][z][n]) with `cnt`: the epilogue's byte counts per
     (row, batch, 4096-column tile) equal the counting kernel's over the stored output
