@@ -25,13 +25,13 @@
 // are stored XOR-swizzled (chunk ^ {0,2,3,1}[(row >> 2) & 3]) so that the 16
 // lanes ds_read_b128 services together (which mix two chunk indices and three
 // row ranges) hit 16 different 16-byte slots of the 256-byte bank row.
-// K = t + k is short (255 -> 4 steps), so the epilogue matters more than the MFMAs
-// (728 clerks x 1000 participants: 288 MFMAs and ~2,200 VALU instructions per wave;
-// the kernel's 26 ms are those two issue streams back to back, 7 + 14 ms). What
-// was tried on it and measured neutral: reductions on the 24-bit multipliers (every
-// 32-bit integer multiply is full rate on this chip), operand reuse through the
-// L2 (the block id remap below), the fold through the double-precision unit (-1 ms
-// with three limbs).
+// K = t + k is short in share generation (255 -> 4 steps), so the epilogue matters as
+// much as the MFMAs, and restaging B for every row block more than either: those
+// shapes go to the panel-resident kernel further down (k_modgemm_panel); this one
+// serves long K (reconstruction over many clerks) and matrices of a few row blocks.
+// What was tried on it and measured neutral: reductions on the 24-bit multipliers
+// (every 32-bit integer multiply is full rate on this chip) and operand reuse through
+// the L2 (the block id remap below).
 //
 // Share generation also needs every sealed box's varint length per 4096-value
 // tile before the encoder can place its bytes (kernels.hpp, launch_count). With
@@ -69,7 +69,7 @@ SDA_DEV int swz(int row, int chunk) {  // position of a row's 16-byte chunk insi
 // Epilogue of a wave's 32 x 16 kJT outputs held as degree sums in `acc` (rows from
 // m_blk + 32 wm, columns from n_blk + 16 kJT wn, C/D map of the 16x16 MFMA): fold,
 // store, and -- with `cnt` -- the byte counts.
-template <typename VT, int kLimbs, int kFold, int kJT, bool kVec>
+template <typename VT, int kLimbs, int kFold, int kJT, bool kVec, int kBlockN>
 __device__ __forceinline__ void gemm_epilogue(const v4i (&acc)[2][kJT][2 * kLimbs - 1], int m_blk, int n_blk,
                                               int z, int wm, int wn, int lane, int M, int N, int batches,
                                               const ModParams& mp, const ModF64& mf, VT* __restrict__ C,
@@ -134,7 +134,7 @@ __device__ __forceinline__ void gemm_epilogue(const v4i (&acc)[2][kJT][2 * kLimb
   // A block whose whole tile is inside the matrix and below `limit` (nine in ten of the
   // share GEMMs' blocks) stores without any per-element test: the tests are a compare
   // or two and a branch per element otherwise.
-  const bool inside = m_blk + kBM <= M && n_blk + kBN <= N && limit < 0 && (!kVec || ldc_n == 1);  // uniform
+  const bool inside = m_blk + kBM <= M && n_blk + kBlockN <= N && limit < 0 && (!kVec || ldc_n == 1);  // uniform
   if (inside) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -174,8 +174,8 @@ __device__ __forceinline__ void gemm_epilogue(const v4i (&acc)[2][kJT][2 * kLimb
       }
   }
   if (cnt == nullptr) return;  // uniform
-  // the block's 128 columns lie inside one count tile (kTileValues is a multiple of kBN)
-  static_assert(kTileValues % kBN == 0, "a block's columns must not straddle a count tile");
+  // the block's columns lie inside one count tile (kTileValues is a multiple of kBlockN)
+  static_assert(kTileValues % kBlockN == 0, "a block's columns must not straddle a count tile");
   const int tile = n_blk / kTileValues;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -312,7 +312,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     if (ks + 1 < nk) commit(cur ^ 1);
     __syncthreads();
   }
-  gemm_epilogue<VT, kLimbs, kFold, 4, false>(acc, m_blk, n_blk, z, wm, wn, lane, M, N, batches, mp, mf, C, ldc_z,
+  gemm_epilogue<VT, kLimbs, kFold, 4, false, kBN>(acc, m_blk, n_blk, z, wm, wn, lane, M, N, batches, mp, mf, C, ldc_z,
                                              ldc_m, ldc_n, limit, cnt, cnt_tiles);
 }
 
@@ -334,46 +334,57 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 // wave's columns: a lane's kJT outputs of a row are neighbours in C and leave in one
 // 16-byte store (the plain order gives 4-byte stores, 64 B runs per instruction; the
 // stores cost 5.5 of the 19 ms).
-// Eight waves: with three limbs two teams of 2 x 2 waves (32 x 64 outputs per wave, 120
+// Eight waves: with three limbs two teams of 2 x 2 waves (32 x 64 outputs per wave, 160
 // accumulator registers) take alternate row blocks; with four limbs one team of 2 x 4
 // (32 x 32 per wave, 112 registers).
+// Where the time goes (728 clerks x 1000 participants, 17.3 ms; the general kernel
+// 26 ms): 8.9 ms of MFMAs per SIMD and ~950 other VALU instructions per wave and tile.
+// The matrix pipe does run under another wave's VALU work (scripts/ubench_mfma_valu.hip)
+// but a single wave issues one VALU instruction every ~6 cycles, not 4, and every MFMA
+// issue costs the other wave ~6 more: by that micro-benchmark's rates this structure
+// ends at ~14 ms. Tried on top and measured neutral: holding the second four waves back
+// half a tile, alternating MFMA and epilogue slots between the two waves of a SIMD
+// under workgroup barriers, raised wave priority in the epilogue, 64-column panels.
+// The fused byte counts cost 1 ms of it (their atomics), filling C alone takes 4.9 ms.
 constexpr int kPanelMaxK = 256;
 
-template <typename VT, int kLimbs, int kFold>
-__global__ void __launch_bounds__(512)
+template <typename VT, int kLimbs, int kFold, int kPN, int kJT, int kTeams>
+__global__ void __launch_bounds__(kPN / (16 * kJT) * 128 * kTeams)
+    __attribute__((amdgpu_waves_per_eu(2, 2)))
     k_modgemm_panel(int M, int N, int Kp, int batches, int gx, int gy, ModParams mp, ModF64 mf,
                     const int8_t* __restrict__ Afrag, const int8_t* __restrict__ B, int64_t b_batch,
                     VT* __restrict__ C, int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit,
                     uint32_t* __restrict__ cnt, int cnt_tiles) {
+  // kPN panel columns, kJT 16-column tiles per wave: kPN / (16 kJT) waves across the
+  // panel, two down the row block, kTeams such teams on alternate row blocks
+  static_assert(kPN % (16 * kJT) == 0, "panel width");
   constexpr int kDeg = 2 * kLimbs - 1;
-  constexpr int kTeams = kLimbs == 3 ? 2 : 1;
-  constexpr int kJT = kLimbs == 3 ? 4 : 2;  // 16-column tiles per wave
+  constexpr int kWavesN = kPN / (16 * kJT);
+  constexpr int kThreads = kWavesN * 128 * kTeams;
   constexpr int kSteps = kPanelMaxK / kBK;
-  constexpr int kPlane = kBN * kBK;         // one (limb, K-step) slab of the panel
+  constexpr int kPlane = kPN * kBK;         // one (limb, K-step) slab of the panel
   __shared__ __attribute__((aligned(16))) int8_t Bs[kLimbs * kSteps * kPlane];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int team = kTeams == 2 ? wave >> 2 : 0;
-  const int wm = kTeams == 2 ? (wave >> 1) & 1 : wave >> 2;
-  const int wn = kTeams == 2 ? wave & 1 : wave & 3;
-  const int n_blk = ((int)blockIdx.x % gx) * kBN, z = (int)blockIdx.x / gx;
+  const int wn = wave % kWavesN, wm = (wave / kWavesN) & 1, team = wave / (2 * kWavesN);
+  const int n_blk = ((int)blockIdx.x % gx) * kPN, z = (int)blockIdx.x / gx;
   const int nk = Kp / kBK;
   {
     // the panel: rows = columns of C, 16-byte pieces; 16 consecutive threads take one
     // row's Kp bytes. All loads are issued before the first LDS write.
     const int8_t* Bz = B + (int64_t)z * (int64_t)N * Kp;
-    const int cpr = Kp / 16, pieces = kLimbs * kBN * cpr;
-    constexpr int kMine = kLimbs * kBN * (kPanelMaxK / 16) / 512;
+    const int cpr = Kp / 16, pieces = kLimbs * kPN * cpr;
+    constexpr int kMine = (kLimbs * kPN * (kPanelMaxK / 16) + kThreads - 1) / kThreads;
     v4i t[kMine];
     int dst[kMine];
 #pragma unroll
     for (int u = 0; u < kMine; ++u) {
-      const int id = u * 512 + tid;
-      const int c = id % cpr, rl = id / cpr, row = rl % kBN, l = rl / kBN;
+      const int id = u * kThreads + tid;
+      const int c = id % cpr, rl = id / cpr, row = rl % kPN, l = rl / kPN;
       // LDS row `row` = tile (row / 16) % kJT, tile column row % 16 of wave row / (16 kJT)
       constexpr int kW = 16 * kJT;
       const int grow = n_blk + (row / kW) * kW + kJT * (row & 15) + ((row >> 4) % kJT);
       const bool ok = id < pieces;
-      dst[u] = ok ? ((l * kSteps + (c >> 2)) * kBN + row) * kBK + 16 * swz(row, c & 3) : -1;
+      dst[u] = ok ? ((l * kSteps + (c >> 2)) * kPN + row) * kBK + 16 * swz(row, c & 3) : -1;
       t[u] = ok && grow < N ? *reinterpret_cast<const v4i*>(Bz + l * b_batch + (int64_t)grow * Kp + 16 * c)
                             : v4i{0, 0, 0, 0};
     }
@@ -382,11 +393,6 @@ __global__ void __launch_bounds__(512)
       if (dst[u] >= 0) *reinterpret_cast<v4i*>(Bs + dst[u]) = t[u];
   }
   __syncthreads();
-  // Waves 0-3 and 4-7 share the four SIMDs pairwise and do identical work: left alone
-  // they stay in step -- both in their MFMAs, then both in their epilogues, each at half
-  // speed, nothing overlapped. Holding the second four back by about one tile's MFMAs
-  // (4,096 cycles) once puts one wave's epilogue under the other's MFMAs from then on.
-  if (wave >= 4) __builtin_amdgcn_s_sleep(64);
 
   const int fr = lane & 15, fg = lane >> 4;
   const int b_off = (wn * (16 * kJT) + fr) * kBK + 16 * swz(fr, fg);
@@ -448,8 +454,8 @@ __global__ void __launch_bounds__(512)
     };
     step(0, std::true_type{});
     for (int ks = 1; ks < nk; ++ks) step(ks, std::false_type{});
-    gemm_epilogue<VT, kLimbs, kFold, kJT, true>(acc, mb * kBM, n_blk, z, wm, wn, lane, M, N, batches, mp, mf, C,
-                                          ldc_z, ldc_m, ldc_n, limit, cnt, cnt_tiles);
+    gemm_epilogue<VT, kLimbs, kFold, kJT, true, kPN>(acc, mb * kBM, n_blk, z, wm, wn, lane, M, N, batches, mp, mf,
+                                                     C, ldc_z, ldc_m, ldc_n, limit, cnt, cnt_tiles);
   }
 }
 
@@ -586,14 +592,26 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
   const bool f64 = p >= 16 && ((g_gemm_fold_f64 == 2 && p < (1u << 24)) || (g_gemm_fold_f64 == 1 && limbs == 3));
   const int fold = f64 && fits53 ? 1 : (p >= (1u << 24) ? 2 : 0);
   const int cnt_tiles = (N + kTileValues - 1) / kTileValues;
-  const int gx = (N + kBN - 1) / kBN, gy = (M + kBM - 1) / kBM;
+  const int gy = (M + kBM - 1) / kBM;
   // short K and enough row blocks to pay for loading the panel
-  if (a_frag != nullptr && Kp <= kPanelMaxK && (int64_t)gx * batches <= 0x7fffffff &&
+  if (a_frag != nullptr && Kp <= kPanelMaxK && (int64_t)((N + 127) / 128) * batches <= 0x7fffffff &&
       (g_gemm_panel > 0 || (g_gemm_panel < 0 && gy >= 4))) {
+    // 128-column panels, eight waves, one workgroup a CU. (64-column panels with two
+    // workgroups a CU, so that one loads its panel while the other computes, measured
+    // the same with 32 x 64 wave tiles and 30 % slower with 32 x 32 ones, which load
+    // every A fragment twice as often.)
+    constexpr int pn = 128;
+    const int gx = (N + pn - 1) / pn;
     dim3 grid((unsigned)(gx * batches));
-#define SDA_PANEL(VT, L, F)                                                                                  \
-  hipLaunchKernelGGL((k_modgemm_panel<VT, L, F>), grid, dim3(512), 0, s, M, N, Kp, batches, gx, gy, mp, mf, a_frag, B, \
-                     b_plane, (VT*)C, ldc_z, ldc_m, ldc_n, limit, cnt, cnt_tiles)
+#define SDA_PANEL_K(VT, L, F, PN, JT, T)                                                                       \
+  hipLaunchKernelGGL((k_modgemm_panel<VT, L, F, PN, JT, T>), grid, dim3(PN / (16 * JT) * 128 * T), 0, s, M, N, Kp, \
+                     batches, gx, gy, mp, mf, a_frag, B, b_plane, (VT*)C, ldc_z, ldc_m, ldc_n, limit, cnt,     \
+                     cnt_tiles)
+#define SDA_PANEL(VT, L, F)                         \
+  do {                                              \
+    if (L == 3) SDA_PANEL_K(VT, 3, F, 128, 4, 2);   \
+    else SDA_PANEL_K(VT, 4, F, 128, 2, 1);          \
+  } while (0)
 #define SDA_PANEL_VT(VT)                                                    \
   do {                                                                      \
     if (limbs == 3) {                                                       \
@@ -611,6 +629,7 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
     else SDA_PANEL_VT(uint32_t);
 #undef SDA_PANEL_VT
 #undef SDA_PANEL
+#undef SDA_PANEL_K
     return;
   }
   GemmGrid gg;

@@ -28,6 +28,18 @@ for c in [int(a) for a in args] or (6, 8):
     X = torch.randint(0, 127, (L, P, B, Kp), dtype=torch.int8, device="cuda")
     out = torch.empty(n, P, B, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(n * P * G.tiles(B), dtype=torch.int32, device="cuda")
+    # the write roofline: the GEMM's output buffer filled by a plain store kernel
+    out.zero_()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(3):
+        out.zero_()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 3
+    print(f"config {c}: filling the {out.numel() * 4 / 1e9:.1f} GB output alone takes {ms:.2f} ms "
+          f"({out.numel() * 4 / ms / 1e9:.2f} TB/s)", flush=True)
     ref = None
     for panel, mode in ((only,) if only else ((0, 0), (0, 2), (1, 0), (1, 2))):
         gpu().set_gemm_fold_f64(mode)

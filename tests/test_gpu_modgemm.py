@@ -22,7 +22,8 @@ def test_modgemm_matches_torch(cuda, prime, fold24, M, N, K, Z, panel):
     """Every epilogue: the 64-bit fold reduced through the double-precision unit (the
     default), and with it switched off the Horner chain of 32-bit Barrett steps
     (p < 2^24) and the 64-bit Barrett fold (p >= 2^24); under the general kernel and,
-    for K <= 256, the panel-resident one (one, two and six row blocks, ragged edges)."""
+    for K <= 256, the panel-resident one (one, two, three and six row blocks, ragged edges,
+    rows of C that start off a 16-byte boundary)."""
     from sda_amd._native import gpu
     from sda_amd.ops import gpu as G
 
