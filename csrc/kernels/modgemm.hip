@@ -490,7 +490,22 @@ __global__ void __launch_bounds__(256)
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int p = blockIdx.y;
   if (gid >= (int64_t)B * groups) return;
-  const int b = (int)(gid / groups), g = (int)(gid % groups);
+  // Groups [g_lo, g_hi) hold random positions and cost a ChaCha block each, the others
+  // a few loads. Threads are numbered with the random groups of all rows first, so a
+  // wave is all generator work or none (row-major, 10 of a row's 16 groups draw with
+  // k = 100, t = 155: three lanes in eight sat idle through every ChaCha block).
+  const int g_lo = k / 16, g_hi = min(groups, (k + t + 15) / 16);
+  const int R = g_hi - g_lo, S = groups - R;
+  int b, g;
+  if (gid < (int64_t)B * R) {
+    b = (int)(gid / R);
+    g = g_lo + (int)(gid % R);
+  } else {
+    const int64_t rest = gid - (int64_t)B * R;
+    b = (int)(rest / S);
+    const int i = (int)(rest % S);
+    g = i < g_lo ? i : i - g_lo + g_hi;
+  }
   RngKey rk;
 #pragma unroll
   for (int i = 0; i < 8; ++i) rk.k[i] = rng.k[i];
