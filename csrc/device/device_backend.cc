@@ -598,16 +598,19 @@ std::vector<int64_t> Backend::reveal(const Aggregation& agg, const EncryptionKey
     } else {
       // large committees: the Lagrange matrix times the results on the int8 matrix cores
       if (m >= (1u << 28)) throw SdaError("GPU backend: packed-Shamir modulus too large for the limb GEMM");
-      const int limbs = m < (1u << 21) ? 3 : 4;
       const int Kp = (nI + 63) / 64 * 64;
+      const LimbScheme sch = limb_scheme(m, Kp);
+      const int limbs = sch.limbs;
       std::vector<int8_t> A((size_t)limbs * k * Kp, 0);
-      for (int l = 0; l < limbs; ++l)
-        for (size_t s = 0; s < k; ++s)
-          for (int i = 0; i < nI; ++i)
-            A[((size_t)l * k + s) * Kp + i] = (int8_t)((lag[s * nI + i] >> (7 * l)) & 0x7f);
+      for (size_t s = 0; s < k; ++s)
+        for (int i = 0; i < nI; ++i) {
+          int8_t d[4];
+          limbs_of_value(lag[s * nI + i], m, sch, d);
+          for (int l = 0; l < limbs; ++l) A[((size_t)l * k + s) * Kp + i] = d[l];
+        }
       int8_t* dA = to_device(mem, A);
       int8_t* X = mem.take<int8_t>((size_t)limbs * B * Kp);
-      launch_limbs_t(nI, (int)B, Kp, limbs, ys, X, s_);
+      launch_limbs_t(nI, (int)B, Kp, m, ys, X, s_);
       launched("limbs_t");
       launch_modgemm_i8((int)k, (int)B, Kp, 1, limbs, m, dA, nullptr, X, (int64_t)B * Kp, 4, masked, 0, 1,
                         (int64_t)k, (int64_t)D, nullptr, s_);
@@ -777,19 +780,22 @@ DeviceParticipations Backend::participate_many(const Aggregation& agg,
         launched("mask_secrets");
         masked = msk;
       }
-      const int limbs = m < (1u << 21) ? 3 : 4;
       const int K = (int)k + t_priv;
       const int Kp = (K + 63) / 64 * 64;
+      const LimbScheme sch = limb_scheme(m, Kp);
+      const int limbs = sch.limbs;
       std::vector<int8_t> A((size_t)limbs * n * Kp, 0);
-      for (int l = 0; l < limbs; ++l)
-        for (int c = 0; c < n; ++c)
-          for (int j = 0; j < K; ++j)
-            A[((size_t)l * n + c) * Kp + j] = (int8_t)((share_matrix[(size_t)c * K + j] >> (7 * l)) & 0x7f);
+      for (int c = 0; c < n; ++c)
+        for (int j = 0; j < K; ++j) {
+          int8_t d[4];
+          limbs_of_value(share_matrix[(size_t)c * K + j], m, sch, d);
+          for (int l = 0; l < limbs; ++l) A[((size_t)l * n + c) * Kp + j] = d[l];
+        }
       int8_t* dA = to_device(mem, A);
       int8_t* dAf = mem.take<int8_t>((size_t)a_fragments_bytes(n, Kp, limbs));
       launch_a_fragments(n, Kp, limbs, dA, dAf, s_);
       int8_t* X = mem.take<int8_t>((size_t)limbs * P * B * Kp);
-      launch_pss_x_limbs(P, (int)D, (int)B, (int)k, t_priv, Kp, limbs, m, masked, rng, 0, X, s_);
+      launch_pss_x_limbs(P, (int)D, (int)B, (int)k, t_priv, Kp, m, masked, rng, 0, X, s_);
       launched("pss_x_limbs");
       // the boxes' varint bytes come out of the GEMM epilogue (cnt zeroed first; this
       // backend never runs inside a captured graph)

@@ -283,26 +283,31 @@ PYBIND11_MODULE(_sda_gpu, m) {
                          int64_t ldc_z, int64_t ldc_m, int64_t ldc_n, int64_t limit,
                          uintptr_t cnt, uintptr_t stream) {
     if (Kp % 64 != 0) throw std::invalid_argument("modgemm_i8: Kp must be a multiple of 64");
-    if (limbs != 3 && limbs != 4) throw std::invalid_argument("modgemm_i8: limbs must be 3 or 4");
-    if (prime >= (1u << (7 * limbs))) throw std::invalid_argument("modgemm_i8: modulus too large");
-    if ((int64_t)Kp * 127 * 127 * limbs >= (int64_t)1 << 31)
+    if (prime < 2 || prime >= (1u << 28)) throw std::invalid_argument("modgemm_i8: modulus must be in [2, 2^28)");
+    if (limbs != limb_scheme(prime, Kp).limbs)
+      throw std::invalid_argument("modgemm_i8: limb count does not match limb_scheme(prime, Kp)");
+    if ((int64_t)Kp * 128 * 128 * limbs >= (int64_t)1 << 31)
       throw std::invalid_argument("modgemm_i8: K too large for int32 limb accumulators");
     launch_modgemm_i8(M, N, Kp, batches, limbs, prime, P<const int8_t>(A), P<const int8_t>(a_frag), P<const int8_t>(B), b_plane,
                       value_bytes, P<void>(C), ldc_z, ldc_m, ldc_n, limit, P<uint32_t>(cnt), S(stream));
     check_launch("modgemm_i8");
   });
-  m.def("pss_x_limbs", [](int Pn, int D, int B, int k, int t, int Kp, int limbs, uint32_t prime,
+  m.def("limb_scheme", [](uint32_t prime, int Kp) {
+    const LimbScheme sch = limb_scheme(prime, Kp);
+    return std::make_pair(sch.limbs, sch.bits);
+  });
+  m.def("pss_x_limbs", [](int Pn, int D, int B, int k, int t, int Kp, uint32_t prime,
                           uintptr_t secrets, std::vector<uint32_t> rng, uint64_t owner_base,
                           uintptr_t X, uintptr_t stream) {
     if (Kp % 64 != 0 || Kp < k + t) throw std::invalid_argument("pss_x_limbs: bad Kp");
-    launch_pss_x_limbs(Pn, D, B, k, t, Kp, limbs, prime, P<const int32_t>(secrets), rng_from(rng),
+    launch_pss_x_limbs(Pn, D, B, k, t, Kp, prime, P<const int32_t>(secrets), rng_from(rng),
                        owner_base, P<int8_t>(X), S(stream));
     check_launch("pss_x_limbs");
   });
-  m.def("limbs_t", [](int R, int N, int Kp, int limbs, uintptr_t Y, uintptr_t out,
+  m.def("limbs_t", [](int R, int N, int Kp, uint32_t prime, uintptr_t Y, uintptr_t out,
                       uintptr_t stream) {
     if (Kp % 64 != 0 || Kp < R) throw std::invalid_argument("limbs_t: bad Kp");
-    launch_limbs_t(R, N, Kp, limbs, P<const uint32_t>(Y), P<int8_t>(out), S(stream));
+    launch_limbs_t(R, N, Kp, prime, P<const uint32_t>(Y), P<int8_t>(out), S(stream));
     check_launch("limbs_t");
   });
   m.def("sub_mod", [](int D, uint32_t mod, uintptr_t a, uintptr_t b, uintptr_t out,

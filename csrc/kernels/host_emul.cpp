@@ -587,6 +587,49 @@ int main() {
       }
     CHECK(ok, "varint length from the leading-zero count");
   }
+  // 7c. the GEMM's signed limb scheme: digits in int8, value recovered, and the fold of
+  //     worst-case and random degree sums (exact integers) against 128-bit arithmetic
+  {
+    uint64_t x = 0x2545f4914f6cdd1dull;
+    auto next = [&x] { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    for (uint32_t m : {(1u << 21), 2097169u, 5038849u, 9999991u, (1u << 24) - (1u << 18) - 1}) {
+      const int Kp = 4096;
+      const LimbScheme sch = limb_scheme(m, Kp);
+      CHECK(sch.limbs == 3 && sch.bits == 8, "limb scheme of m=%u", m);
+      bool ok = true;
+      for (int it = 0; it < 200000 && ok; ++it) {
+        uint32_t v = (uint32_t)(next() % m);
+        if (it < 8) v = (uint32_t[]){0u, 1u, m / 2, m / 2 + 1, m - 1, m / 2 - 1, 255u, 65535u}[it];
+        int8_t d[4];
+        limbs_of_value(v, m, sch, d);
+        const int64_t back = (int64_t)d[0] + 256 * (int64_t)d[1] + 65536 * (int64_t)d[2];
+        ok = ((back % (int64_t)m) + m) % m == v && (back == (int64_t)v || back == (int64_t)v - (int64_t)m);
+      }
+      CHECK(ok, "signed limbs of m=%u", m);
+      const ModF64 P = make_modf64_signed(m, Kp);
+      const int64_t top[5] = {(int64_t)Kp << 14, (int64_t)Kp << 15, 3 * ((int64_t)Kp << 14), (int64_t)Kp << 15,
+                              (int64_t)Kp << 14};  // |acc_d| at most
+      for (int it = 0; it < 200000 && ok; ++it) {
+        int64_t a[5];
+        for (int dgr = 0; dgr < 5; ++dgr) {
+          const int mode = it < 64 ? (it >> dgr) & 1 : 2;  // all sign patterns of the extremes first
+          a[dgr] = mode == 2 ? (int64_t)(next() % (2 * (uint64_t)top[dgr] + 1)) - top[dgr]
+                             : (mode ? top[dgr] : -top[dgr]);
+        }
+        double s = P.off + (double)a[0];
+        s = __builtin_fma((double)a[1], 256.0, s);
+        s = __builtin_fma((double)a[2], 65536.0, s);
+        s = __builtin_fma((double)a[3], 16777216.0, s);
+        s = __builtin_fma((double)a[4], P.w4, s);
+        __int128 ref = 0;
+        for (int dgr = 4; dgr >= 0; --dgr) ref = ref * 256 + a[dgr];
+        int64_t r = (int64_t)(ref % (__int128)m);
+        if (r < 0) r += m;
+        ok = s >= 0 && s < 0x1p53 && modf64d(s, P) == (uint32_t)r;
+      }
+      CHECK(ok, "signed-limb fold m=%u", m);
+    }
+  }
   // 8. the encode kernel's packed varint pairs against a plain zigzag-LEB128 encoder:
   //    every low value with a spread of high values, and the reverse
   {

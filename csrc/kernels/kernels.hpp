@@ -242,8 +242,34 @@ void launch_sub_mod(int D, uint32_t m, const uint32_t* a, const uint32_t* b, uin
                     hipStream_t s);
 
 // ---- modgemm.hip -----------------------------------------------------------
-// C = A . B mod p (p < 2^28) on i8 MFMA with `limbs` (3 or 4) 7-bit limbs. A limbs
-// [L][M][Kp], B limbs [L][batches][N][Kp] (b_plane = batches*N*Kp bytes between limb
+// How field elements become int8 GEMM operands: `limbs` digits of `bits` bits -- 7:
+// non-negative base-128 digits of the canonical value; 8: signed base-256 digits of the
+// balanced residue (three limbs; 2^21 <= p < 2^24 - 2^18 and Kp <= 4096).
+struct LimbScheme {
+  int limbs, bits;
+};
+inline LimbScheme limb_scheme(uint32_t p, int Kp) {
+  if (p < (1u << 21)) return LimbScheme{3, 7};
+  // signed digits: the top one stays inside int8 for p / 2 + 128 + 2^15 <= 127 * 2^16; the
+  // fold's sums (below K 2^40 each way) stay exact in doubles for K <= 4096
+  if (p < (1u << 24) - (1u << 18) && Kp <= 4096) return LimbScheme{3, 8};
+  return LimbScheme{4, 7};
+}
+// The limbs d[0 .. limbs) of one canonical value (host side: the fixed A operands).
+inline void limbs_of_value(uint32_t x, uint32_t p, LimbScheme sch, int8_t* d) {
+  if (sch.bits == 7) {
+    for (int l = 0; l < sch.limbs; ++l) d[l] = (int8_t)((x >> (7 * l)) & 0x7f);
+    return;
+  }
+  int32_t t = x > p / 2 ? (int32_t)x - (int32_t)p : (int32_t)x;
+  for (int l = 0; l + 1 < sch.limbs; ++l) {
+    d[l] = (int8_t)(t & 0xff);
+    t = (t - d[l]) >> 8;
+  }
+  d[sch.limbs - 1] = (int8_t)t;
+}
+// C = A . B mod p (p < 2^28) on i8 MFMA, operands in limb_scheme(p, Kp) (`limbs` must be
+// its limb count). A limbs [L][M][Kp], B limbs [L][batches][N][Kp] (b_plane = batches*N*Kp bytes between limb
 // planes), C[z*ldc_z + m*ldc_m + n*ldc_n] written where that index < limit.
 // cnt (may be null; zeroed by the caller): [M][batches][ceil(N / kTileValues)] varint
 // bytes of the written elements, i.e. launch_count's result for C as M x batches
@@ -264,12 +290,10 @@ void set_gemm_fold_f64(int mode);
 // -1 (default): the panel-resident kernel for short K with at least four row blocks;
 // 0 never; 1 whenever Kp <= 256 (both need a_frag)
 void set_gemm_panel(int mode);
-// X limbs [3][P][B][Kp] of packed-Shamir inputs: secrets (canonical) then t draws.
-void launch_pss_x_limbs(int P, int D, int B, int k, int t, int Kp, int limbs, uint32_t p,
-                        const int32_t* secrets, RngKeyArg rng, uint64_t owner_base, int8_t* X,
-                        hipStream_t s);
-// Limbs of Y [R][N] transposed to [3][N][Kp].
-void launch_limbs_t(int R, int N, int Kp, int limbs, const uint32_t* Y, int8_t* out,
-                    hipStream_t s);
+// X limbs [L][P][B][Kp] of packed-Shamir inputs: secrets (canonical) then t draws.
+void launch_pss_x_limbs(int P, int D, int B, int k, int t, int Kp, uint32_t p, const int32_t* secrets,
+                        RngKeyArg rng, uint64_t owner_base, int8_t* X, hipStream_t s);
+// Limbs of Y [R][N] (canonical values) transposed to [L][N][Kp].
+void launch_limbs_t(int R, int N, int Kp, uint32_t p, const uint32_t* Y, int8_t* out, hipStream_t s);
 
 }  // namespace sdagpu

@@ -67,9 +67,22 @@ SDA_DEV uint32_t mod24(uint32_t w, const Mod24& P) {
 // instructions, whatever v's size -- a 64-bit Barrett step (mod64) takes about thirty.
 struct ModF64 {
   double m, inv;
+  double off, w4;  // the signed-limb fold of the modular GEMM: a multiple of m above its sums, 2^32 mod m
 };
 inline ModF64 make_modf64(uint32_t m) {
-  return ModF64{(double)m, m ? (1.0 / (double)m) * (1.0 - 0x1p-50) : 0.0};
+  return ModF64{(double)m, m ? (1.0 / (double)m) * (1.0 - 0x1p-50) : 0.0, 0.0, 0.0};
+}
+// The same for the modular GEMM's signed-limb fold (three signed base-256 limbs, K-sums
+// of up to Kp products): |sum_d acc_d w_d| <= Kp 128^2 (w4 + 2 2^24 + 3 2^16 + 2 2^8 + 1)
+// with w4 = 2^32 mod m; `off`, the next multiple of m, lifts the sum to [0, 2^53) for
+// Kp <= 4096 and m < 2^24.
+inline ModF64 make_modf64_signed(uint32_t m, int Kp) {
+  ModF64 P = make_modf64(m);
+  const uint64_t w4 = (1ull << 32) % m;
+  const uint64_t bound = (uint64_t)Kp * 16384 * (w4 + (2ull << 24) + (3ull << 16) + (2ull << 8) + 1);
+  P.off = (double)((bound + m - 1) / m * m);
+  P.w4 = (double)w4;
+  return P;
 }
 // v given as a double (an exact integer below 2^53)
 SDA_DEV uint32_t modf64d(double vd, const ModF64& P) {

@@ -4,11 +4,15 @@
 // K = t + k = 255 inputs, n = 728 shares, p = 746497; PSS_155_19682_100) turns
 // share generation into S = M . X (n x K times K x batches, per participant) and
 // reconstruction into L_I . Y (k x |I| times |I| x batches).
-// Values are split into L = 3 (p < 2^21) or 4 (p < 2^28) 7-bit limbs (int8,
-// non-negative), so every limb product fits the i8 MFMA and a K-sum of up to L
-// limb products per degree stays below 2^31 (K * 127^2 * L < 2^31). The L^2
-// limb products per K-step go into 2L - 1 accumulators by degree d = i + j;
-// the epilogue folds sum_d acc_d 2^(7d) mod p (kFold below).
+// Values are split into int8 limbs (limb_scheme): L = 3 (p < 2^21) or 4 (p < 2^28)
+// non-negative 7-bit digits, or -- 2^21 <= p < 2^24 - 2^18, K <= 4096 -- three signed
+// base-256 digits of the balanced residue (|x| <= p / 2): the i8 MFMA multiplies signed
+// bytes, and nine products per K-step and five degree sums instead of sixteen and seven
+// is what the 19,682-clerk field (p = 5,038,849) saves by it. Every limb product fits
+// the MFMA and a K-sum of up to L limb products per degree stays inside 32 bits
+// (K * 127^2 * L, K * 128^2 * L < 2^31). The L^2 limb products per K-step go into
+// 2L - 1 accumulators by degree d = i + j; the epilogue folds sum_d acc_d 2^(b d) mod p
+// (b = 7 or 8; kFold below).
 //
 // Layouts: A limbs [L][M][Kp] (row-major, k contiguous), B limbs
 // [L][batch][N][Kp] (B stored transposed: each column contiguous in k); Kp is a
@@ -64,7 +68,10 @@ SDA_DEV int swz(int row, int chunk) {  // position of a row's 16-byte chunk insi
 // caller checks sum < 2^53), degrees 3..6 first and then the rest with four. 0: a
 // Horner chain of 32-bit Barrett steps (p < 2^24: s < p and acc_d < 2^31 keep
 // s * 2^7 + acc_d below 2^32). 2: 64-bit multiply-adds by 2^(7d) mod p and one 64-bit
-// Barrett reduction (any p < 2^28). 0 and 2 are the integer-only references.
+// Barrett reduction (any p < 2^28). 0 and 2 are the integer-only references. 3: signed
+// base-256 limbs (three of them): sum_d acc_d w_d in doubles with w_d = 2^(8 d) for
+// d < 4 and 2^32 mod p for d = 4, plus a multiple of p that makes the sum positive --
+// one reduction: every term is below K 2^40 in size and K <= 4096.
 //
 // Epilogue of a wave's 32 x 16 kJT outputs held as degree sums in `acc` (rows from
 // m_blk + 32 wm, columns from n_blk + 16 kJT wn, C/D map of the 16x16 MFMA): fold,
@@ -94,7 +101,15 @@ __device__ __forceinline__ void gemm_epilogue(const v4i (&acc)[2][kJT][2 * kLimb
   const int64_t step_j = kColStep * ldc_n, step_i = 16 * ldc_m;
   uint32_t bytes[2][2] = {{0, 0}, {0, 0}};  // varint bytes of rows (i, r): two 16-bit sums per word
   auto fold = [&](int i, int j, int r) -> uint32_t {
-    if constexpr (kFold == 1) {
+    if constexpr (kFold == 3) {
+      static_assert(kFold != 3 || kLimbs == 3, "signed limbs come in threes");
+      double s = mf.off + (double)acc[i][j][0][r];
+      s = __builtin_fma((double)acc[i][j][1][r], 256.0, s);
+      s = __builtin_fma((double)acc[i][j][2][r], 65536.0, s);
+      s = __builtin_fma((double)acc[i][j][3][r], 16777216.0, s);
+      s = __builtin_fma((double)acc[i][j][4][r], mf.w4, s);
+      return modf64d(s, mf);
+    } else if constexpr (kFold == 1) {
       // neighbouring degrees pair up in 32 bits (acc_d 2^7 + acc_(d-1) < 2^32: the
       // caller's bound on K), the pairs meet as doubles: exact integers below 2^53
       auto pair = [&](int d) -> double {  // acc_(d+1) 2^7 + acc_d, or acc_d alone at the top
@@ -459,20 +474,42 @@ __global__ void __launch_bounds__(kPN / (16 * kJT) * 128 * kTeams)
   }
 }
 
-template <int kLimbs>
-SDA_DEV void put_limbs(int8_t* dst, int64_t plane, const uint32_t (&v)[16]) {
+// Sixteen canonical values -> their limbs, 16 bytes per limb plane. kBits == 7: the
+// non-negative base-128 digits. kBits == 8 (three limbs): the signed base-256 digits of
+// the balanced residue x - (x > p / 2 ? p : 0): d0 = low byte as int8, then the same of
+// (x - d0) >> 8, and what is left (|.| <= 128 by limb_scheme's bound on p).
+template <int kLimbs, int kBits>
+SDA_DEV void put_limbs(int8_t* dst, int64_t plane, const uint32_t (&v)[16], uint32_t p) {
+  uint32_t q[kLimbs][4];
 #pragma unroll
-  for (int l = 0; l < kLimbs; ++l) {
-    uint32_t q[4];
+  for (int u = 0; u < 4; ++u) {
+    uint32_t x[kLimbs];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      uint32_t x = 0;
+    for (int l = 0; l < kLimbs; ++l) x[l] = 0;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) x |= ((v[4 * u + b] >> (kLimbBits * l)) & 0x7fu) << (8 * b);
-      q[u] = x;
+    for (int b = 0; b < 4; ++b) {
+      if constexpr (kBits == 7) {
+#pragma unroll
+        for (int l = 0; l < kLimbs; ++l) x[l] |= ((v[4 * u + b] >> (kLimbBits * l)) & 0x7fu) << (8 * b);
+      } else {
+        static_assert(kBits == 7 || kLimbs == 3, "signed limbs come in threes");
+        int32_t t = (int32_t)v[4 * u + b];
+        if ((uint32_t)t > (p >> 1)) t -= (int32_t)p;
+        const int32_t d0 = (int32_t)(int8_t)(t & 0xff);
+        t = (t - d0) >> 8;
+        const int32_t d1 = (int32_t)(int8_t)(t & 0xff);
+        t = (t - d1) >> 8;
+        x[0] |= ((uint32_t)d0 & 0xffu) << (8 * b);
+        x[1] |= ((uint32_t)d1 & 0xffu) << (8 * b);
+        x[2] |= ((uint32_t)t & 0xffu) << (8 * b);
+      }
     }
-    *reinterpret_cast<uint4*>(dst + l * plane) = make_uint4(q[0], q[1], q[2], q[3]);
+#pragma unroll
+    for (int l = 0; l < kLimbs; ++l) q[l][u] = x[l];
   }
+#pragma unroll
+  for (int l = 0; l < kLimbs; ++l)
+    *reinterpret_cast<uint4*>(dst + l * plane) = make_uint4(q[l][0], q[l][1], q[l][2], q[l][3]);
 }
 
 // X limbs of packed-Shamir share generation: row b of participant p is
@@ -481,7 +518,7 @@ SDA_DEV void put_limbs(int8_t* dst, int64_t plane, const uint32_t (&v)[16]) {
 // (b * Kp/16 + j/16) of the participant's share stream (exact uniform with the
 // retry stream for rejected words), so every draw is a pure function of
 // (round key, participant, batch, position).
-template <int kLimbs>
+template <int kLimbs, int kBits>
 __global__ void __launch_bounds__(256)
     k_pss_x_limbs(int P, int D, int B, int k, int t, int Kp, ModParams mp,
                   const int32_t* __restrict__ secrets, RngKeyArg rng, uint64_t owner_base,
@@ -531,14 +568,14 @@ __global__ void __launch_bounds__(256)
     v[i] = x;
   }
   const int64_t plane = (int64_t)P * B * Kp;
-  put_limbs<kLimbs>(X + ((int64_t)p * B + b) * Kp + j0, plane, v);
+  put_limbs<kLimbs, kBits>(X + ((int64_t)p * B + b) * Kp + j0, plane, v, mp.m);
 }
 
 // Limbs of a [R][N] u32 matrix, transposed to [3][N][Kp] (Kp >= R, zero padded):
 // the B operand of reconstruction (rows = surviving clerks, columns = batches).
-template <int kLimbs>
+template <int kLimbs, int kBits>
 __global__ void __launch_bounds__(256)
-    k_limbs_t(int R, int N, int Kp, const uint32_t* __restrict__ Y, int8_t* __restrict__ out) {
+    k_limbs_t(int R, int N, int Kp, uint32_t p, const uint32_t* __restrict__ Y, int8_t* __restrict__ out) {
   const int groups = Kp / 16;
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (int64_t)N * groups) return;
@@ -549,7 +586,7 @@ __global__ void __launch_bounds__(256)
     const int r = 16 * g + i;
     v[i] = r < R ? Y[(int64_t)r * N + col] : 0u;
   }
-  put_limbs<kLimbs>(out + (int64_t)col * Kp + 16 * g, (int64_t)N * Kp, v);
+  put_limbs<kLimbs, kBits>(out + (int64_t)col * Kp + 16 * g, (int64_t)N * Kp, v, p);
 }
 
 // A limbs [L][M][Kp] in the order the panel kernel's waves load them: [row block]
@@ -591,7 +628,9 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
                        hipStream_t s) {
   if (M <= 0 || N <= 0 || batches <= 0) return;
   ModParams mp = make_mod_params(p);
-  const ModF64 mf = make_modf64(p);
+  ModF64 mf = make_modf64(p);
+  const LimbScheme sch = limb_scheme(p, Kp);
+  if (sch.limbs != limbs) return;  // the operands were not made for this field (callers check)
   // no truncation: the per-element bound check goes away (the kernel takes limit < 0)
   if ((int64_t)(batches - 1) * ldc_z + (int64_t)(M - 1) * ldc_m + (int64_t)(N - 1) * ldc_n < limit &&
       ldc_z >= 0 && ldc_m >= 0 && ldc_n >= 0)
@@ -605,7 +644,11 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
   // chain: three limbs 28.9 -> 27.8 ms, four limbs 21.0 -> 20.4 ms (four limbs: the
   // second stage's r 2^28 + ... stays below 2^53 only for p < 2^24)
   const bool f64 = p >= 16 && ((g_gemm_fold_f64 == 2 && p < (1u << 24)) || (g_gemm_fold_f64 == 1 && limbs == 3));
-  const int fold = f64 && fits53 ? 1 : (p >= (1u << 24) ? 2 : 0);
+  int fold = f64 && fits53 ? 1 : (p >= (1u << 24) ? 2 : 0);
+  if (sch.bits == 8) {
+    fold = 3;
+    mf = make_modf64_signed(p, Kp);
+  }
   const int cnt_tiles = (N + kTileValues - 1) / kTileValues;
   const int gy = (M + kBM - 1) / kBM;
   // short K and enough row blocks to pay for loading the panel
@@ -622,28 +665,28 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
   hipLaunchKernelGGL((k_modgemm_panel<VT, L, F, PN, JT, T>), grid, dim3(PN / (16 * JT) * 128 * T), 0, s, M, N, Kp, \
                      batches, gx, gy, mp, mf, a_frag, B, b_plane, (VT*)C, ldc_z, ldc_m, ldc_n, limit, cnt,     \
                      cnt_tiles)
-#define SDA_PANEL(VT, L, F)                         \
-  do {                                              \
-    if (L == 3) SDA_PANEL_K(VT, 3, F, 128, 4, 2);   \
-    else SDA_PANEL_K(VT, 4, F, 128, 2, 1);          \
-  } while (0)
+#define SDA_PANEL3(VT, F) SDA_PANEL_K(VT, 3, F, 128, 4, 2)
+#define SDA_PANEL4(VT, F) SDA_PANEL_K(VT, 4, F, 128, 2, 1)
 #define SDA_PANEL_VT(VT)                                                    \
   do {                                                                      \
     if (limbs == 3) {                                                       \
-      if (fold == 1) SDA_PANEL(VT, 3, 1); else SDA_PANEL(VT, 3, 0);         \
+      if (fold == 3) SDA_PANEL3(VT, 3);                                     \
+      else if (fold == 1) SDA_PANEL3(VT, 1);                                \
+      else SDA_PANEL3(VT, 0);                                               \
     } else if (fold == 2) {                                                 \
-      SDA_PANEL(VT, 4, 2);                                                  \
+      SDA_PANEL4(VT, 2);                                                    \
     } else if (fold == 1) {                                                 \
-      SDA_PANEL(VT, 4, 1);                                                  \
+      SDA_PANEL4(VT, 1);                                                    \
     } else {                                                                \
-      SDA_PANEL(VT, 4, 0);                                                  \
+      SDA_PANEL4(VT, 0);                                                    \
     }                                                                       \
   } while (0)
     if (value_bytes == 1) SDA_PANEL_VT(uint8_t);
     else if (value_bytes == 2) SDA_PANEL_VT(uint16_t);
     else SDA_PANEL_VT(uint32_t);
 #undef SDA_PANEL_VT
-#undef SDA_PANEL
+#undef SDA_PANEL3
+#undef SDA_PANEL4
 #undef SDA_PANEL_K
     return;
   }
@@ -670,7 +713,9 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
 #define SDA_GEMM_VT(VT)                                                     \
   do {                                                                      \
     if (limbs == 3) {                                                       \
-      if (fold == 1) SDA_GEMM(VT, 3, 1); else SDA_GEMM(VT, 3, 0);           \
+      if (fold == 3) SDA_GEMM(VT, 3, 3);                                    \
+      else if (fold == 1) SDA_GEMM(VT, 3, 1);                               \
+      else SDA_GEMM(VT, 3, 0);                                              \
     } else if (fold == 2) {                                                 \
       SDA_GEMM(VT, 4, 2);                                                   \
     } else if (fold == 1) {                                                 \
@@ -686,29 +731,24 @@ void launch_modgemm_i8(int M, int N, int Kp, int batches, int limbs, uint32_t p,
 #undef SDA_GEMM
 }
 
-void launch_pss_x_limbs(int P, int D, int B, int k, int t, int Kp, int limbs, uint32_t p,
-                        const int32_t* secrets, RngKeyArg rng, uint64_t owner_base, int8_t* X,
-                        hipStream_t s) {
+void launch_pss_x_limbs(int P, int D, int B, int k, int t, int Kp, uint32_t p, const int32_t* secrets,
+                        RngKeyArg rng, uint64_t owner_base, int8_t* X, hipStream_t s) {
   if (P <= 0 || B <= 0) return;
   const int64_t threads = (int64_t)B * (Kp / 16);
   dim3 grid((unsigned)((threads + 255) / 256), P);
-  if (limbs == 3)
-    hipLaunchKernelGGL(k_pss_x_limbs<3>, grid, dim3(256), 0, s, P, D, B, k, t, Kp,
-                       make_mod_params(p), secrets, rng, owner_base, X);
-  else
-    hipLaunchKernelGGL(k_pss_x_limbs<4>, grid, dim3(256), 0, s, P, D, B, k, t, Kp,
-                       make_mod_params(p), secrets, rng, owner_base, X);
+  const LimbScheme sch = limb_scheme(p, Kp);
+  auto kern = sch.bits == 8 ? k_pss_x_limbs<3, 8> : sch.limbs == 3 ? k_pss_x_limbs<3, 7> : k_pss_x_limbs<4, 7>;
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, P, D, B, k, t, Kp, make_mod_params(p), secrets, rng,
+                     owner_base, X);
 }
 
-void launch_limbs_t(int R, int N, int Kp, int limbs, const uint32_t* Y, int8_t* out,
-                    hipStream_t s) {
+void launch_limbs_t(int R, int N, int Kp, uint32_t p, const uint32_t* Y, int8_t* out, hipStream_t s) {
   if (R <= 0 || N <= 0) return;
   const int64_t threads = (int64_t)N * (Kp / 16);
   dim3 grid((unsigned)((threads + 255) / 256));
-  if (limbs == 3)
-    hipLaunchKernelGGL(k_limbs_t<3>, grid, dim3(256), 0, s, R, N, Kp, Y, out);
-  else
-    hipLaunchKernelGGL(k_limbs_t<4>, grid, dim3(256), 0, s, R, N, Kp, Y, out);
+  const LimbScheme sch = limb_scheme(p, Kp);
+  auto kern = sch.bits == 8 ? k_limbs_t<3, 8> : sch.limbs == 3 ? k_limbs_t<3, 7> : k_limbs_t<4, 7>;
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, R, N, Kp, p, Y, out);
 }
 
 }  // namespace sdagpu

@@ -16,11 +16,12 @@ def main():
     ps = PSS_155_728_100
     p, n, K = ps.prime_modulus, ps.share_count, ps.secret_count + ps.privacy_threshold_
     P, B = 64, 10000  # participants x batches (1M dims / 100 secrets per batch)
-    Kp, L = G.padded_k(K), G.limb_count(p)
+    Kp = G.padded_k(K)
+    L = G.limb_count(p, Kp)
     dev = torch.device("cuda")
     g = torch.Generator(device="cuda").manual_seed(1)
     A = torch.randint(0, p, (n, K), dtype=torch.int32, device=dev, generator=g)
-    Al = G.limbs_of(A, Kp, L)
+    Al = G.limbs_of(A, Kp, p)
     X = torch.randint(0, 128, (L, P, B, Kp), dtype=torch.int8, device=dev, generator=g)
     out = torch.empty(n, P, B, dtype=torch.int32, device=dev)
 

@@ -23,8 +23,9 @@ for c in [int(a) for a in args] or (6, 8):
     ps = cfg.sharing()
     p, n, K = ps.field_modulus, ps.share_count, ps.secret_count + ps.privacy_threshold_
     P, B = cfg.participants, cfg.dimension // ps.secret_count
-    L, Kp = G.limb_count(p), G.padded_k(K)
-    A = torch.randint(0, 127, (L, n, Kp), dtype=torch.int8, device="cuda")
+    Kp = G.padded_k(K)
+    L = G.limb_count(p, Kp)
+    A = torch.randint(0, 127, (L, n, Kp), dtype=torch.int8, device="cuda")  # any digits time alike
     X = torch.randint(0, 127, (L, P, B, Kp), dtype=torch.int8, device="cuda")
     out = torch.empty(n, P, B, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(n * P * G.tiles(B), dtype=torch.int32, device="cuda")

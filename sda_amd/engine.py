@@ -176,11 +176,11 @@ class DeviceAggregator:
             # matrix cores (int8-limb MFMA GEMM) for the large parameter sets
             self._pss_mfma = pss_backend == "mfma" or (pss_backend == "auto" and big)
             if self._pss_mfma:
-                self._limbs = G.limb_count(self.m)
                 self._Kp = G.padded_k(ps.secret_count + ps.privacy_threshold_)
+                self._limbs = G.limb_count(self.m, self._Kp)
                 self._M_limbs = G.limbs_of(
                     self._share_matrix.view(self.n, ps.secret_count + ps.privacy_threshold_),
-                    self._Kp, self._limbs)
+                    self._Kp, self.m)
                 self._M_frag = G.a_fragments(self._M_limbs) if self._Kp <= G.PANEL_MAX_K else None
         else:
             self._pss = None
@@ -579,7 +579,7 @@ class DeviceAggregator:
                                           out_dtype=torch.int32) for r in rows])
             if self._pss_mfma:
                 lag_limbs, kp = self._lagrange_limbs(live)
-                G.modgemm_i8(lag_limbs, G.limbs_t(ys, kp, self._limbs), m, masked, ldc_z=0,
+                G.modgemm_i8(lag_limbs, G.limbs_t(ys, kp, m), m, masked, ldc_z=0,
                              ldc_m=1, ldc_n=spec.sharing.secret_count, limit=D)
             else:
                 lag = self._lagrange(live)
@@ -641,7 +641,7 @@ class DeviceAggregator:
         if key not in cache:
             kp = G.padded_k(len(live))
             lag = self._lagrange(live).view(self.spec.sharing.secret_count, len(live))
-            cache[key] = (G.limbs_of(lag, kp, self._limbs), kp)
+            cache[key] = (G.limbs_of(lag, kp, self.m), kp)
         return cache[key]
 
     def _lagrange(self, live):

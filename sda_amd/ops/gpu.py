@@ -491,22 +491,38 @@ def padded_k(K: int) -> int:
     return (K + 63) // 64 * 64
 
 
-def limb_count(prime: int) -> int:
-    """7-bit limbs per element: 3 for p < 2^21, 4 for p < 2^28."""
-    if prime < 2 ** 21:
-        return 3
-    if prime < 2 ** 28:
-        return 4
-    raise ValueError("modgemm: modulus must be < 2^28")
+def limb_scheme(prime: int, Kp: int) -> tuple[int, int]:
+    """(limbs, bits) of the GEMM operands for this field and (padded) K: 7-bit non-negative
+    digits (3 limbs for p < 2^21, 4 for p < 2^28) or, for 2^21 <= p < 2^24 - 2^18 and
+    K <= 4096, three signed base-256 digits of the balanced residue."""
+    if not 2 <= prime < 2 ** 28:
+        raise ValueError("modgemm: modulus must be in [2, 2^28)")
+    return tuple(_gpu().limb_scheme(prime, Kp))
 
 
-def limbs_of(values: torch.Tensor, Kp: int, limbs: int) -> torch.Tensor:
-    """Limb planes [L][rows][Kp] (int8) of a [rows][K] matrix of field elements."""
+def limb_count(prime: int, Kp: int) -> int:
+    return limb_scheme(prime, Kp)[0]
+
+
+def limbs_of(values: torch.Tensor, Kp: int, prime: int) -> torch.Tensor:
+    """Limb planes [L][rows][Kp] (int8) of a [rows][K] matrix of canonical field elements,
+    in limb_scheme(prime, Kp)."""
+    if prime < 16:
+        raise ValueError("limbs_of takes the modulus (the limb count follows from it)")
     rows, K = values.shape
+    limbs, bits = limb_scheme(prime, Kp)
     v = values.to(torch.int64)
     out = torch.zeros(limbs, rows, Kp, dtype=torch.int8, device=values.device)
-    for l in range(limbs):
-        out[l, :, :K] = ((v >> (7 * l)) & 0x7F).to(torch.int8)
+    if bits == 7:
+        for l in range(limbs):
+            out[l, :, :K] = ((v >> (7 * l)) & 0x7F).to(torch.int8)
+        return out
+    v = torch.where(v > prime // 2, v - prime, v)  # balanced residue
+    for l in range(limbs - 1):
+        d = ((v & 0xFF) ^ 0x80) - 0x80  # low byte as int8
+        out[l, :, :K] = d.to(torch.int8)
+        v = (v - d) >> 8
+    out[limbs - 1, :, :K] = v.to(torch.int8)
     return out
 
 
@@ -538,7 +554,7 @@ def modgemm_i8(A_limbs: torch.Tensor, B_limbs: torch.Tensor, prime: int, out: to
     _check(B_limbs, "B_limbs", torch.int8)
     L, M, Kp = A_limbs.shape
     Lb, Z, N, Kb = B_limbs.shape
-    if Kb != Kp or Lb != L or L != limb_count(prime):
+    if Kb != Kp or Lb != L or L != limb_count(prime, Kp):
         raise ValueError("limb shape mismatch")
     vb = value_bytes(out.dtype)
     if out.dtype == torch.uint8 and prime > 256:
@@ -568,17 +584,19 @@ def pss_x_limbs(secrets: torch.Tensor, k: int, t: int, prime: int, rng_key: byte
     _check(secrets, "secrets", torch.int32)
     B = (D + k - 1) // k
     Kp = padded_k(k + t)
-    L = limb_count(prime)
+    L = limb_count(prime, Kp)
     X = torch.empty(L, P, B, Kp, dtype=torch.int8, device=secrets.device)
-    _gpu().pss_x_limbs(P, D, B, k, t, Kp, L, prime, _ptr(secrets), rng_words(rng_key), owner_base,
+    _gpu().pss_x_limbs(P, D, B, k, t, Kp, prime, _ptr(secrets), rng_words(rng_key), owner_base,
                        _ptr(X), _stream())
     return X
 
 
-def limbs_t(Y: torch.Tensor, Kp: int, limbs: int) -> torch.Tensor:
-    """Limbs of Y [R][N] (int32 field elements) transposed to [L][1][N][Kp]."""
+def limbs_t(Y: torch.Tensor, Kp: int, prime: int) -> torch.Tensor:
+    """Limbs of Y [R][N] (int32 canonical field elements) transposed to [L][1][N][Kp]."""
+    if prime < 16:
+        raise ValueError("limbs_t takes the modulus (the limb count follows from it)")
     R, N = Y.shape
     _check(Y, "Y", torch.int32)
-    out = torch.empty(limbs, 1, N, Kp, dtype=torch.int8, device=Y.device)
-    _gpu().limbs_t(R, N, Kp, limbs, _ptr(Y), _ptr(out), _stream())
+    out = torch.empty(limb_count(prime, Kp), 1, N, Kp, dtype=torch.int8, device=Y.device)
+    _gpu().limbs_t(R, N, Kp, prime, _ptr(Y), _ptr(out), _stream())
     return out

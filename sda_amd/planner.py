@@ -135,8 +135,9 @@ def participant_bytes(spec: AggregationSpec, pss_backend: str = "auto",
     mfma = uses_mfma(spec, pss_backend)
     if mfma:
         ps = spec.sharing
-        limbs = 3 if m < 2 ** 21 else 4
         kp = _round_up(ps.secret_count + ps.privacy_threshold_, 64)
+        # the GEMM's limb_scheme: three limbs (7-bit, or signed 8-bit up to 2^24 - 2^18), else four
+        limbs = 3 if m < 2 ** 21 or (m < 2 ** 24 - 2 ** 18 and kp <= 4096) else 4
         short += limbs * B * kp                              # X limb planes
     if isinstance(spec.masking, FullMask):
         held += _box_bytes(D, m, True)

@@ -10,8 +10,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("prime,fold24", [(746497, 1), (746497, 0), (5038849, 2), (5038849, 0),
-                                          (433, 1), (433, 0), (16777213, 2), (16777213, 1),
+@pytest.mark.parametrize("prime,fold24", [(746497, 1), (746497, 0), (5038849, 2), (2097169, 2),
+                                          ((1 << 24) - (1 << 18) - 1, 2),
+                                          (433, 1), (433, 0), (16777213, 2), (16777213, 1), (16777213, 0),
                                           ((1 << 27) - 39, 2), ((1 << 27) - 39, 0),
                                           ((1 << 28) - 57, 2)])
 @pytest.mark.parametrize("M,N,K,Z,panel", [(37, 45, 100, 2, 0), (64, 64, 64, 1, 0), (5, 300, 255, 3, 0),
@@ -19,9 +20,11 @@ pytestmark = pytest.mark.gpu
                                            (5, 300, 255, 3, 1), (333, 200, 190, 2, 1), (130, 301, 100, 2, 1),
                                            (64, 128, 64, 1, 1)])
 def test_modgemm_matches_torch(cuda, prime, fold24, M, N, K, Z, panel):
-    """Every epilogue: the 64-bit fold reduced through the double-precision unit (the
-    default), and with it switched off the Horner chain of 32-bit Barrett steps
-    (p < 2^24) and the 64-bit Barrett fold (p >= 2^24); under the general kernel and,
+    """Every limb scheme and epilogue: three signed base-256 limbs (2^21 <= p < 2^24 - 2^18,
+    both ends of that range); 7-bit limbs with the 64-bit fold reduced through the
+    double-precision unit (the default) and, with it switched off, the Horner chain of
+    32-bit Barrett steps (p < 2^24) and the 64-bit Barrett fold (p >= 2^24); under the
+    general kernel and,
     for K <= 256, the panel-resident one (one, two, three and six row blocks, ragged edges,
     rows of C that start off a 16-byte boundary)."""
     from sda_amd._native import gpu
@@ -30,10 +33,9 @@ def test_modgemm_matches_torch(cuda, prime, fold24, M, N, K, Z, panel):
     g = torch.Generator().manual_seed(M * N + K)
     A = torch.randint(0, prime, (M, K), generator=g, dtype=torch.int64)
     Bm = torch.randint(0, prime, (Z, N, K), generator=g, dtype=torch.int64)  # B stored transposed
-    L = G.limb_count(prime)
     Kp = G.padded_k(K)
-    Al = G.limbs_of(A.to(torch.int32).cuda(), Kp, L)
-    Bl = torch.stack([G.limbs_of(Bm[z].to(torch.int32).cuda(), Kp, L) for z in range(Z)], 1)
+    Al = G.limbs_of(A.to(torch.int32).cuda(), Kp, prime)
+    Bl = torch.stack([G.limbs_of(Bm[z].to(torch.int32).cuda(), Kp, prime) for z in range(Z)], 1)
     out = torch.zeros(Z * M * N, dtype=torch.int32, device="cuda")
     gpu().set_gemm_fold_f64(fold24)
     gpu().set_gemm_panel(panel)
@@ -51,11 +53,12 @@ def test_modgemm_matches_torch(cuda, prime, fold24, M, N, K, Z, panel):
 
 
 @pytest.mark.parametrize("panel", [0, 1])
-def test_modgemm_transposed_truncated_store(cuda, panel):
+@pytest.mark.parametrize("p", [746497, 5038849, (1 << 27) - 39])  # limbs_t in every scheme
+def test_modgemm_transposed_truncated_store(cuda, panel, p):
     from sda_amd._native import gpu
     from sda_amd.ops import gpu as G
 
-    p, k, R, N = 746497, 100, 255, 40
+    k, R, N = 100, 255, 40
     g = torch.Generator().manual_seed(3)
     Lm = torch.randint(0, p, (k, R), generator=g, dtype=torch.int64)
     Y = torch.randint(0, p, (R, N), generator=g, dtype=torch.int64)
@@ -64,12 +67,12 @@ def test_modgemm_transposed_truncated_store(cuda, panel):
     out = torch.full((D,), -1, dtype=torch.int32, device="cuda")
     gpu().set_gemm_panel(panel)
     try:
-        G.modgemm_i8(G.limbs_of(Lm.to(torch.int32).cuda(), Kp, 3),
-                     G.limbs_t(Y.to(torch.int32).cuda(), Kp, 3), p, out, ldc_z=0, ldc_m=1, ldc_n=k,
+        G.modgemm_i8(G.limbs_of(Lm.to(torch.int32).cuda(), Kp, p),
+                     G.limbs_t(Y.to(torch.int32).cuda(), Kp, p), p, out, ldc_z=0, ldc_m=1, ldc_n=k,
                      limit=D)
     finally:
         gpu().set_gemm_panel(-1)
-    ref = ((Lm @ Y) % p).T.reshape(-1)[:D]
+    ref = (sum((Lm[:, i:i + 1] * Y[i:i + 1, :]) % p for i in range(R)) % p).T.reshape(-1)[:D]
     assert torch.equal(out.cpu().to(torch.int64), ref)
 
 
@@ -90,10 +93,9 @@ def test_modgemm_epilogue_counts_varint_bytes(cuda, prime, dtype, M, N, Z, panel
     A = torch.randint(0, prime, (M, K), generator=g, dtype=torch.int64)
     Bm = torch.randint(0, prime, (Z, N, K), generator=g, dtype=torch.int64)
     Bm[:, ::5] = 0  # short codes too: whole output columns of zeros
-    L = G.limb_count(prime)
     Kp = G.padded_k(K)
-    Al = G.limbs_of(A.to(torch.int32).cuda(), Kp, L)
-    Bl = torch.stack([G.limbs_of(Bm[z].to(torch.int32).cuda(), Kp, L) for z in range(Z)], 1)
+    Al = G.limbs_of(A.to(torch.int32).cuda(), Kp, prime)
+    Bl = torch.stack([G.limbs_of(Bm[z].to(torch.int32).cuda(), Kp, prime) for z in range(Z)], 1)
     out = torch.zeros(M, Z, N, dtype=dtype, device="cuda")
     T = G.tiles(N)
     cnt = torch.zeros(M * Z * T, dtype=torch.int32, device="cuda")
@@ -137,13 +139,13 @@ def test_round_pss_155_728_100_dropout_fullmask(cuda):
     _round(AggregationSpec(777, p, PSS_155_728_100, FullMask(p)), 2, clerks=live)
 
 
-def test_round_pss_155_19682_100_four_limbs(cuda):
+def test_round_pss_155_19682_100_signed_limbs(cuda):
     from sda_amd.models import PSS_155_19682_100, AggregationSpec
 
     spec = AggregationSpec(150, PSS_155_19682_100.prime_modulus, PSS_155_19682_100)
     # 19682 clerks; reconstruct from 300 of them (t + k = 255 needed)
     agg = _round(spec, 1, clerks=list(range(0, 600, 2)))
-    assert agg._limbs == 4
+    assert agg._limbs == 3  # p = 5,038,849: three signed base-256 limbs
 
 
 def test_pss_4_8_3_mfma_backend_matches(cuda):

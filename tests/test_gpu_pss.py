@@ -119,9 +119,9 @@ def test_fft_model_shares_reconstruct_on_device(cuda, name):
         out = torch.empty(D, dtype=torch.int32, device="cuda")
         G.pss_reconstruct(ys, lag, k, D, p, out)
         assert torch.equal(out.cpu().to(torch.int64), want), live
-        kp, limbs = G.padded_k(len(live)), G.limb_count(p)
+        kp = G.padded_k(len(live))
         out2 = torch.full((D,), -1, dtype=torch.int32, device="cuda")
-        G.modgemm_i8(G.limbs_of(lag.view(k, len(live)), kp, limbs), G.limbs_t(ys, kp, limbs), p,
+        G.modgemm_i8(G.limbs_of(lag.view(k, len(live)), kp, p), G.limbs_t(ys, kp, p), p,
                      out2, ldc_z=0, ldc_m=1, ldc_n=k, limit=D)
         assert torch.equal(out2.cpu().to(torch.int64), want), live
 
