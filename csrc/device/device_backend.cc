@@ -495,7 +495,7 @@ void Backend::seal_data(Lease& mem, const Arena& a, const Keys& k, const void* v
   launch_segscan(M, T, cnt, a.pt_len, 0, nullptr, s_);  // tile byte offsets; pt_len = totals
   launched("segscan");
   launch_encode_encrypt(M, L, value_bytes, values, cnt, k.keys, a.ct, a.stride, nullptr, nullptr,
-                        nullptr, 0, s_);
+                        nullptr, 0, varint_max_len(a.modulus), s_);
   launched("encode_encrypt");
   if (short_boxes(a)) {
     launch_mac_short(M, k.keys, k.pows, a.ct, a.stride, a.pt_len, 0, nullptr, err, s_);

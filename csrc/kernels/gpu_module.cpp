@@ -164,10 +164,11 @@ PYBIND11_MODULE(_sda_gpu, m) {
   });
   m.def("encode_encrypt", [](int M, int L, int value_bytes, uintptr_t vals, uintptr_t tile_off,
                              uintptr_t keys, uintptr_t ct, uint64_t stride, uintptr_t pows,
-                             uintptr_t pt_len, uintptr_t partials, int K, uintptr_t stream) {
+                             uintptr_t pt_len, uintptr_t partials, int K, int max_code_bytes,
+                             uintptr_t stream) {
     launch_encode_encrypt(M, L, value_bytes, P<const void>(vals), P<const uint32_t>(tile_off),
                           P<const MsgKey>(keys), P<uint8_t>(ct), stride, P<const uint32_t>(pows),
-                          P<const uint32_t>(pt_len), P<uint32_t>(partials), K, S(stream));
+                          P<const uint32_t>(pt_len), P<uint32_t>(partials), K, max_code_bytes, S(stream));
     check_launch("encode_encrypt");
   });
   m.def("poly_powers", [](int M, uintptr_t keys, uintptr_t pows, int full, uintptr_t stream) {

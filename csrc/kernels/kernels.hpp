@@ -169,10 +169,13 @@ void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, uint32_t exp
 // every tile also adds its share of the Poly1305 partials of the message's middle
 // chunks (all but the first and the last) to `partials`; launch_mac_edges then
 // supplies those two and launch_mac_final the tag.
+// max_code_bytes: the longest varint the values can have (5 = any u32; the arena's slots
+// are sized by the same bound): 32-bit values with at most 3 / 4 bytes get a kernel
+// with a smaller LDS tile and more workgroups per CU.
 void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
                            const uint32_t* tile_off, const MsgKey* keys, uint8_t* ct,
                            uint64_t stride, const uint32_t* pows, const uint32_t* pt_len,
-                           uint32_t* partials, int K, hipStream_t s);
+                           uint32_t* partials, int K, int max_code_bytes, hipStream_t s);
 // Poly1305 partials of every message's first and last chunk only (per-lane Horner).
 void launch_mac_edges(int M, int K, const MsgKey* keys, const uint32_t* pows, const uint8_t* ct,
                       uint64_t stride, const uint32_t* pt_len, uint32_t* partials, hipStream_t s);

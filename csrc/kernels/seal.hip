@@ -93,14 +93,20 @@ SDA_DEV void load_values(uint32_t (&v)[kValuesPerLane], const VT* src, int e0, i
 //   row value  = (sum_pos u_pos W(pos) + row constant + pad bits of the owned blocks)
 //   chunk part = sum_i row value_i * r^(16 - i)     (relative to the chunk's end, as
 //                                                    k_mac_chunks' middle chunks are)
-template <typename VT, bool MAC>
+// kMaxB: the longest code the caller's values can have (u8 / u16 storage: 3; u32: 3 for
+// values below 2^20, 4 below 2^27, else 5). It sizes the tile's LDS -- 24 / 32 / 40 KB,
+// i.e. six / four / three workgroups a CU; the issue-bound kernel ran at 57 % of its
+// VALU peak with three -- and a value past the bound (a caller's error: the slots of
+// the arena are sized by the same bound) is encoded as zero rather than overrun it.
+template <typename VT, bool MAC, int kMaxB>
 __global__ void __launch_bounds__(kBlock)
     k_encode_encrypt(int L, const VT* __restrict__ vals, const uint32_t* __restrict__ tile_off,
                      const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct, uint64_t stride,
                      const uint32_t* __restrict__ pows, const uint32_t* __restrict__ pt_len,
                      uint32_t* __restrict__ partials, int K) {
-  // u16 values are at most 3-byte varints, u32 at most 5
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kEncodeValues * (sizeof(VT) <= 2 ? 3 : 5) + 128];
+  static_assert(kMaxB >= 3 && kMaxB <= 5 && (sizeof(VT) > 2 || kMaxB == 3), "code length bound");
+  constexpr uint32_t kBound = kMaxB == 5 ? 0xffffffffu : (1u << (7 * kMaxB - 1)) - 1u;  // largest value
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kEncodeValues * kMaxB + 128];
   __shared__ uint32_t scratch[kWaves];
   // chunks a tile can touch: its bytes span at most 2 + (tile bytes - 2) / chunk bytes
   constexpr int kSlots = sizeof(VT) <= 2 ? 3 : 4;
@@ -157,14 +163,19 @@ __global__ void __launch_bounds__(kBlock)
       load_values<VT>(v, src, e0, L);
 #pragma unroll
       for (int i = 0; i < kValuesPerLane; ++i) orv |= v[i];
+      if (kMaxB < 5 && orv > kBound) {  // never with canonical values
+#pragma unroll
+        for (int i = 0; i < kValuesPerLane; ++i) v[i] = 0;
+        orv = 0;
+      }
     }
     fast = full && orv < 8192u;
     if (fast) {
 #pragma unroll
       for (int i = 0; i < kValuesPerLane; ++i) my_bytes += 1u + (v[i] >= 64u);
     }
-    mid = !fast && full && orv < (1u << 27);
-    mid3 = mid && orv < (1u << 20);
+    mid = !fast && full && (kMaxB < 5 || orv < (1u << 27));
+    mid3 = mid && (kMaxB == 3 || orv < (1u << 20));
   }
   // value i of the lane on the generic paths
   auto val = [&](int i) -> uint32_t {
@@ -183,7 +194,7 @@ __global__ void __launch_bounds__(kBlock)
       const uint32_t z = val(i) << 1;
       my_bytes += 1u + (z >= (1u << 7)) + (z >= (1u << 14)) + (z >= (1u << 21));
     }
-  } else if (!fast && full) {
+  } else if (kMaxB == 5 && !fast && full) {
 #pragma unroll
     for (int i = 0; i < kValuesPerLane; ++i) {
       const uint64_t z = (uint64_t)val(i) << 1;
@@ -192,7 +203,8 @@ __global__ void __launch_bounds__(kBlock)
   } else if (!fast) {
 #pragma unroll 1
     for (int i = 0; i < nv; ++i) {
-      const uint64_t z = (uint64_t)src[e0 + i] << 1;
+      const uint32_t x = (uint32_t)src[e0 + i];
+      const uint64_t z = (uint64_t)(x > kBound ? 0u : x) << 1;
       my_bytes += 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
     }
   }
@@ -258,7 +270,7 @@ __global__ void __launch_bounds__(kBlock)
       if (i + 3 < kValuesPerLane || l3) lds[pos + 3] = (uint8_t)(z >> 21);
       pos += 1u + l1 + l2 + l3;
     }
-  } else if (full) {
+  } else if (kMaxB == 5 && full) {
 #pragma unroll
     for (int i = 0; i < kValuesPerLane; ++i) {
       const uint64_t z = (uint64_t)val(i) << 1;
@@ -272,7 +284,8 @@ __global__ void __launch_bounds__(kBlock)
   } else {
 #pragma unroll 1
     for (int i = 0; i < nv; ++i) {
-      const uint64_t z = (uint64_t)src[e0 + i] << 1;
+      const uint32_t x = (uint32_t)src[e0 + i];
+      const uint64_t z = (uint64_t)(x > kBound ? 0u : x) << 1;
       const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
 #pragma unroll
       for (int q = 0; q < 5; ++q)
@@ -1087,30 +1100,34 @@ void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, uint32_t exp
   hipLaunchKernelGGL(k_segscan, dim3(M), dim3(kBlock), 0, s, T, data, totals, expect, err);
 }
 
-template <typename VT>
+template <typename VT, int kMaxB>
 static void launch_encode_t(dim3 grid, int L, const void* vals, const uint32_t* tile_off,
                             const MsgKey* keys, uint8_t* ct, uint64_t stride, const uint32_t* pows,
                             const uint32_t* pt_len, uint32_t* partials, int K, hipStream_t s) {
   if (pows && pt_len && partials)
-    hipLaunchKernelGGL((k_encode_encrypt<VT, true>), grid, dim3(kBlock), 0, s, L, (const VT*)vals,
-                       tile_off, keys, ct, stride, pows, pt_len, partials, K);
+    hipLaunchKernelGGL((k_encode_encrypt<VT, true, (sizeof(VT) > 2 ? 5 : 3)>), grid, dim3(kBlock), 0, s, L,
+                       (const VT*)vals, tile_off, keys, ct, stride, pows, pt_len, partials, K);
   else
-    hipLaunchKernelGGL((k_encode_encrypt<VT, false>), grid, dim3(kBlock), 0, s, L, (const VT*)vals,
+    hipLaunchKernelGGL((k_encode_encrypt<VT, false, kMaxB>), grid, dim3(kBlock), 0, s, L, (const VT*)vals,
                        tile_off, keys, ct, stride, pows, pt_len, partials, K);
 }
 
 void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
                            const uint32_t* tile_off, const MsgKey* keys, uint8_t* ct,
                            uint64_t stride, const uint32_t* pows, const uint32_t* pt_len,
-                           uint32_t* partials, int K, hipStream_t s) {
+                           uint32_t* partials, int K, int max_code_bytes, hipStream_t s) {
   if (M <= 0 || L <= 0) return;
   dim3 grid((L + kEncodeValues - 1) / kEncodeValues, M);
   if (value_bytes == 1)
-    launch_encode_t<uint8_t>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
+    launch_encode_t<uint8_t, 3>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
   else if (value_bytes == 2)
-    launch_encode_t<uint16_t>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
+    launch_encode_t<uint16_t, 3>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
+  else if (max_code_bytes <= 3)
+    launch_encode_t<uint32_t, 3>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
+  else if (max_code_bytes == 4)
+    launch_encode_t<uint32_t, 4>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
   else
-    launch_encode_t<uint32_t>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
+    launch_encode_t<uint32_t, 5>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
 }
 
 extern int g_powers_prio;  // keys.hip (set_key_prio)

@@ -273,11 +273,13 @@ def segscan(data: torch.Tensor, totals: torch.Tensor | None, expect: int | None 
                    int(expect or 0) & 0xFFFFFFFF, e, _stream())
 
 
-def encode_encrypt(vals, tile_off, keys, ct, stride, mac=None):
+def encode_encrypt(vals, tile_off, keys, ct, stride, mac=None, max_code_bytes=5):
     """Varint-encode + encrypt the rows of `vals` into the arena. `mac` =
     (pows, pt_len, partials, K) fuses the Poly1305 of the middle chunks into the
     pass (`partials` zeroed); :func:`mac_edges` and :func:`mac_final` complete
-    the tag."""
+    the tag. `max_code_bytes`: :func:`varint_max_len` of the values' modulus (the
+    bound the arena's slots are sized by); 32-bit values of at most 3 / 4 bytes
+    run with a smaller LDS tile and more workgroups per CU."""
     M, L = vals.shape
     _check(vals, "vals", VALUE_DTYPES)
     _check(tile_off, "tile_off", torch.int32, numel=M * tiles(L))
@@ -292,7 +294,7 @@ def encode_encrypt(vals, tile_off, keys, ct, stride, mac=None):
         _check(t_part, "partials", torch.int32, numel=M * K * 8)
         pows, pt_len, partials = _ptr(t_pows), _ptr(t_len), _ptr(t_part)
     _gpu().encode_encrypt(M, L, value_bytes(vals.dtype), _ptr(vals), _ptr(tile_off), _ptr(keys),
-                          _ptr(ct), stride, pows, pt_len, partials, K, _stream())
+                          _ptr(ct), stride, pows, pt_len, partials, K, int(max_code_bytes), _stream())
 
 
 def poly_powers(M, keys, pows, full=True):

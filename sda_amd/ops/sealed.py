@@ -201,7 +201,8 @@ def seal_encode(arena: Arena, keys: KeySet, values: torch.Tensor,
         G.encode_encrypt(values, cnt, keys.keys, arena.ct, arena.stride,
                          mac=(keys.pows, arena.pt_len, partials, arena.K))
     else:
-        G.encode_encrypt(values, cnt, keys.keys, arena.ct, arena.stride)
+        G.encode_encrypt(values, cnt, keys.keys, arena.ct, arena.stride,
+                         max_code_bytes=G.varint_max_len(arena.modulus))
     return keys, partials
 
 
