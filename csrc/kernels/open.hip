@@ -254,7 +254,7 @@ SDA_DEV uint32_t spread4(uint32_t bits4) {  // 4 bits -> 0xff per set bit, byte 
 // nearly all two bytes (m > 2048), not for the small moduli with their mix of one-
 // and two-byte codes (irregular strides already).
 template <int kMaxBytes, bool kSwz>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMaxBytes > 2 ? 3 : 4)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
     k_decode_sum_z(int L, int P, int Pg, const uint8_t* __restrict__ pt, uint64_t stride,
                    const uint32_t* __restrict__ pt_len, int S, const uint32_t* __restrict__ pre,
                    const uint32_t* __restrict__ tile_sub, uint32_t* __restrict__ part,
