@@ -60,13 +60,11 @@ int chunks_for(size_t max_pt) { return (int)((max_pt + 32 + kChunkBytes - 1) / k
 int tiles(size_t L) { return (int)((L + kTileValues - 1) / kTileValues); }
 int sum_tiles(size_t L) { return (int)((L + kSumTile - 1) / kSumTile); }
 
-// most participants one u32 decode-sum accumulator may add up
+// most participants one decode-sum accumulator may add up (64-bit accumulators above 2^27)
 uint64_t decode_sum_group_limit(uint64_t m) {
-  uint64_t per;
-  if (m <= 8192) per = 16383;
-  else if (m <= (1ull << 27)) per = 2 * (m - 1) < (1ull << 21) ? (1ull << 21) - 1 : (1ull << 28) - 1;
-  else per = m - 1;
-  return std::max<uint64_t>(1, 0xffffffffull / std::max<uint64_t>(1, per));
+  if (m > (1ull << 27)) return 1ull << 30;
+  const uint64_t per = m <= 8192 ? 16383 : 2 * (m - 1) < (1ull << 21) ? (1ull << 21) - 1 : (1ull << 28) - 1;
+  return std::max<uint64_t>(1, 0xffffffffull / per);
 }
 int decode_group_size(int P, int tiles_x_rows, uint64_t limit) {
   auto cdiv = [](int a, int b) { return (a + b - 1) / b; };
@@ -465,7 +463,7 @@ void Backend::open_sum(Lease& mem, const Arena& a, const Keys& k, int rows, uint
   launched("locate_tiles");
   const int Pg = decode_group_size(P, T * rows, decode_sum_group_limit(a.modulus));
   const int G = (P + Pg - 1) / Pg;
-  uint32_t* part = mem.take<uint32_t>((size_t)G * rows * L);
+  uint32_t* part = mem.take<uint32_t>((size_t)G * rows * L * (decode_sum_wide((uint32_t)a.modulus) ? 2 : 1));
   uint32_t* redo = zeros(mem, 1);
   launch_decode_sum(rows, P, Pg, L, a.modulus, a.ct, a.stride, a.pt_len, S, pre, tile_sub, part, out,
                     nullptr, err, redo, s_);

@@ -9,7 +9,8 @@
 //   put(local, v, term)   every byte position; `term` = 1 where a value ends
 //                         (the sink routes term = 0 to a dummy slot, so the
 //                         unrolled loop stays branch-free)
-//   put_rank(rank, v)     a long varint (>= 4 bytes) recovered by the slow walk
+//   put_rank(rank, v)     a varint whose code does not fit 32 bits (six bytes and more,
+//                         or a fifth byte above 15) recovered by the slow walk
 //   kAdditive             the sink accumulates (an aborted fast pass is undone
 //                         by re-adding its values negated); additive sinks also
 //   put_masked(local, v)  take every position's value pre-masked (0 where no
@@ -171,14 +172,15 @@ SDA_DEV bool decode_canon(const uint32_t (&w)[16], uint32_t prev_word, uint64_t 
 }
 
 // Decodes the varints terminated in one lane's 64 bytes.
-//   w, prev_word  the bytes and the 4 bytes before them (message order)
-//   tmask, traw   valid terminators / raw terminator bits of all 64 bytes
-//   local         block-local rank of the lane's first valid terminator
-//   gmsg, p0      the message in global memory and the lane's first position
-//                 (long varints walk back through it)
+//   w                       the lane's bytes (message order)
+//   prev_word2, prev_word   the 8 bytes before them (bytes -8..-5 and -4..-1)
+//   tmask, traw             valid terminators / raw terminator bits of all 64 bytes
+//   local                   block-local rank of the lane's first valid terminator
+//   gmsg, p0                the message in global memory and the lane's first position
+//                           (codes beyond 32 bits walk back through it)
 // Returns true if the stream is malformed.
 template <bool kFast16, typename Sink>
-SDA_DEV bool decode_lane(const uint32_t (&w)[16], uint32_t prev_word, uint64_t tmask,
+SDA_DEV bool decode_lane(const uint32_t (&w)[16], uint32_t prev_word2, uint32_t prev_word, uint64_t tmask,
                          uint64_t traw, uint32_t local, const ModParams& mp,
                          const uint8_t* __restrict__ gmsg, int64_t p0, Sink& sink) {
   bool bad = false;
@@ -231,49 +233,69 @@ SDA_DEV bool decode_lane(const uint32_t (&w)[16], uint32_t prev_word, uint64_t t
     }
   }
   if (redo) {
-    // Generic path, all in registers. A terminator at b closes a 1-, 2- or
-    // 3-byte varint depending on the continuation bits of bytes b-1, b-2; four
-    // bytes and more (|value| >= 2^20) take the walk below.
+    // Generic path, all in registers: one pass over the bytes carrying the code of the
+    // continuation run so far (`run`, its length as a shift `sh`). A terminator closes
+    // the code run | byte << sh; codes of up to five bytes that fit 32 bits (every
+    // canonical value of a modulus up to 2^31) end here, anything longer or larger is
+    // flagged (`ovf`) and left to the walk below. The state before the lane's first byte
+    // comes from the eight bytes before it; eight continuation bytes there mean a run
+    // that began out of sight: flagged too.
     // opaque copies: stop the compiler from sharing (and keeping live across
     // the fast path) the per-byte terms it would otherwise CSE between paths
     uint32_t tlo = (uint32_t)tmask, thi = (uint32_t)(tmask >> 32);
     local = local0;
     asm volatile("" : "+v"(tlo), "+v"(thi), "+v"(local));
     uint32_t long_mask_lo = 0, long_mask_hi = 0;  // terminators needing the slow path
-    uint32_t b3 = (prev_word >> 8) & 0xffu, b2 = (prev_word >> 16) & 0xffu, b1 = prev_word >> 24;
     // Conditions are kept as integer 0/1 / all-ones masks (bools become SGPR
     // lane masks that the compiler then spills across the unrolled loop).
+    uint32_t run = 0, sh = 0, ovf = 0;
+    uint32_t z = 0;
+    auto step = [&](uint32_t byte) {  // z = the code ending at `byte`; then the state after it
+      const uint32_t cm = (uint32_t)((int32_t)(byte << 24) >> 31);  // all ones: continuation byte
+      const uint64_t s64 = (uint64_t)(byte & 0x7fu) << sh;           // sh <= 35
+      z = run | (uint32_t)s64;
+      ovf |= (uint32_t)(s64 >> 32);
+      const uint32_t flagged = ovf;
+      uint32_t nsh = (sh + 7u) & cm;
+      nsh = nsh < 35u ? nsh : 35u;
+      run = z & cm;
+      ovf = (ovf & cm) | (nsh >> 5);  // five continuation bytes in a row: six bytes or more
+      sh = nsh;
+      return flagged;
+    };
+    {
+      uint32_t allc = 1;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t byte = ((i < 4 ? prev_word2 : prev_word) >> (8 * (i & 3))) & 0xffu;
+        (void)step(byte);
+        allc &= byte >> 7;
+      }
+      ovf |= allc;
+    }
     uint32_t neg_raw = 0;
 #pragma unroll
     for (int b = 0; b < 64; ++b) {
       const uint32_t byte = (w[b >> 2] >> (8 * (b & 3))) & 0xffu;
       const uint32_t term = ((b < 32 ? tlo : thi) >> (b & 31)) & 1u;
-      const uint32_t c1 = b1 >> 7, c2 = b2 >> 7, c3 = b3 >> 7;
-      const uint32_t m1 = 0u - c1, m2 = 0u - c2;
-      const uint32_t z2 = (b1 & 0x7f) | (byte << 7);
-      const uint32_t z3 = (b2 & 0x7f) | ((b1 & 0x7f) << 7) | (byte << 14);
-      const uint32_t z = (byte & ~m1) | (z2 & m1 & ~m2) | (z3 & m1 & m2);  // < 2^21
-      const uint32_t lng = term & c1 & c2 & c3;
+      const uint32_t lng = term & (step(byte) != 0u ? 1u : 0u);
       if (b < 32) long_mask_lo |= lng << b; else long_mask_hi |= lng << (b - 32);
       const uint32_t neg = z & 1u;
-      const uint32_t u = (z >> 1) + neg;  // |value| (value = -u when neg)
+      const uint32_t u = (z >> 1) + neg;  // |value| (value = -u when neg), at most 2^31
       const uint32_t r = mod32(u, mp);    // m == 0: raw
       const uint32_t nr = r == 0 ? 0u : mp.m - r;
       const uint32_t v = r ^ ((r ^ nr) & (0u - neg));
       neg_raw |= term & neg & (lng ^ 1u);
-      sink.put(local, v, term & (lng ^ 1u));  // long varints: written by the walk
+      sink.put(local, v, term & (lng ^ 1u));  // flagged codes: written by the walk
       local += term;
-      b3 = b2;
-      b2 = b1;
-      b1 = byte;
     }
     if (mp.m == 0) bad |= neg_raw != 0;  // a raw (modulus-free) stream holds no negatives
-    // rare slow path: values of >= 4-byte varints
+    // rare slow path: codes that do not fit 32 bits
     uint64_t lm = ((uint64_t)long_mask_hi << 32) | long_mask_lo;
     while (lm) {
       const int b = __builtin_ctzll(lm);
       lm &= lm - 1;
-      const uint32_t r = local0 + (uint32_t)__popcll(tmask & ((1ull << b) - 1));
+      const uint32_t r = local0 + (uint32_t)__builtin_popcountll(tmask & ((1ull << b) - 1));
       const int64_t q = p0 + b;
       int64_t s0 = q;
       int n = 0;

@@ -241,7 +241,7 @@ PYBIND11_MODULE(_sda_gpu, m) {
                          uintptr_t stream) {
     if (mod == 0) throw std::invalid_argument("decode_sum: needs a modulus");
     if (out == 0 && acc == 0) throw std::invalid_argument("decode_sum: needs out or acc");
-    if ((uint64_t)Pg * (mod - 1) > 0xffffffffull)
+    if (!decode_sum_wide(mod) && (uint64_t)Pg * (mod - 1) > 0xffffffffull)
       throw std::invalid_argument("decode_sum: Pg * (m - 1) overflows the u32 accumulators");
     // lean kernels add zigzag codes: up to 14 bits (two bytes), 21 (three) or 28 (four)
     const uint64_t code_max = mod <= 8192u ? 16383ull

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <vector>
 
+#include "decode_core.hpp"
 #include "device_crypto.hpp"
 #include "kernels.hpp"
 #include "modarith.hpp"
@@ -337,6 +338,18 @@ static void emul_mac_fused(uint32_t (&tag)[4], const MsgKey& key, const uint8_t*
   p130_finish(tag, H, s4);
 }
 
+// sink of the host run of decode_lane: values by rank, and how often each rank was written
+struct HostDecodeSink {
+  static constexpr bool kAdditive = false;
+  std::vector<uint32_t>* out;
+  std::vector<int>* hits;
+  void put(uint32_t local, uint32_t v, uint32_t term) {
+    if (term) { (*out)[local] = v; ++(*hits)[local]; }
+  }
+  void put_masked(uint32_t local, uint32_t v) { put(local, v, 1); }
+  void put_rank(uint32_t rank, uint32_t v) { (*out)[rank] = v; ++(*hits)[rank]; }
+};
+
 int main() {
   // 1. primitives vs host
   for (int it = 0; it < 20; ++it) {
@@ -628,6 +641,86 @@ int main() {
         ok = s >= 0 && s < 0x1p53 && modf64d(s, P) == (uint32_t)r;
       }
       CHECK(ok, "signed-limb fold m=%u", m);
+    }
+  }
+  // 7d. the generic varint decoder, lane by lane as the kernels call it (64 bytes a lane,
+  //     the 8 bytes before it, terminator masks, ranks), against a plain decoder: codes of
+  //     one to five bytes, negative values, values past the modulus, overlong and
+  //     64-bit codes (the walk), for small and the largest moduli and for raw u32 output
+  {
+    using HostSink = HostDecodeSink;
+    uint64_t x = 0x853c49e6748fea9bull;
+    auto next = [&x] { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    for (uint32_t m : {433u, 746497u, 5038849u, (1u << 27) - 39, 2147483647u, 0u}) {
+      const ModParams mp = make_mod_params(m);
+      for (int variant = 0; variant < 3; ++variant) {
+        // variant 0: canonical values; 1: mixed lengths and signs; 2: with overlong / huge codes
+        std::vector<uint8_t> msg;
+        std::vector<uint32_t> want;
+        const int count = 3000;
+        for (int i = 0; i < count; ++i) {
+          int64_t v;
+          const uint64_t r = next();
+          const uint64_t span = m ? m : 0xffffffffull;
+          if (variant == 0) v = (int64_t)(r % span);
+          else {
+            const int bits = 1 + (int)((r >> 40) % (variant == 2 ? 62 : 31));
+            v = (int64_t)(r & ((1ull << bits) - 1));
+            if (m != 0 && (r >> 63)) v = -v;
+            if (m == 0) v &= 0xffffffffll;
+          }
+          uint64_t z = ((uint64_t)v << 1) ^ (uint64_t)(v >> 63);
+          int pad = variant == 2 && (r >> 50) % 7 == 0 ? 1 + (int)((r >> 53) % 3) : 0;  // overlong: zero groups
+          int len = 1;
+          for (uint64_t t = z >> 7; t; t >>= 7) ++len;
+          if (len + pad > 10) pad = 10 - len;  // ten bytes is the longest code the decoders take
+          do {
+            uint8_t b = z & 0x7f;
+            z >>= 7;
+            if (z || pad) b |= 0x80;
+            msg.push_back(b);
+          } while (z);
+          while (pad--) msg.push_back(pad ? 0x80 : 0x00);
+          uint32_t ref;
+          if (m == 0) ref = (uint32_t)v;
+          else {
+            int64_t t = v % (int64_t)m;
+            ref = (uint32_t)(t < 0 ? t + m : t);
+          }
+          want.push_back(ref);
+        }
+        const int64_t N = (int64_t)msg.size();
+        msg.resize(msg.size() + 128, 0);
+        std::vector<uint32_t> got(want.size(), 0xdeadbeefu);
+        std::vector<int> hits(want.size(), 0);
+        HostSink sink{&got, &hits};
+        uint32_t rank = 0;
+        bool bad = false;
+        for (int64_t p0 = 0; p0 < N; p0 += 64) {
+          uint32_t w[16];
+          for (int q = 0; q < 16; ++q) {
+            uint32_t word = 0;
+            for (int b = 0; b < 4; ++b) {
+              const int64_t pos = p0 + 4 * q + b;
+              word |= (uint32_t)(pos < N ? msg[pos] : 0) << (8 * b);
+            }
+            w[q] = word;
+          }
+          auto word_at = [&](int64_t pos) {
+            uint32_t word = 0;
+            if (pos >= 0) std::memcpy(&word, &msg[pos], 4);
+            return word;
+          };
+          const int hi = (int)std::min<int64_t>(64, N - p0);
+          const uint64_t traw = term_mask64(w);
+          const uint64_t tmask = traw & byte_range_mask(0, hi);
+          bad |= decode_lane<false>(w, word_at(p0 - 8), word_at(p0 - 4), tmask, traw, rank, mp, msg.data(), p0, sink);
+          rank += (uint32_t)__builtin_popcountll(tmask);
+        }
+        bool ok = rank == want.size() && !bad;
+        for (size_t i = 0; i < want.size() && ok; ++i) ok = got[i] == want[i] && hits[i] == 1;
+        CHECK(ok, "generic varint decode m=%u variant %d", m, variant);
+      }
     }
   }
   // 8. the encode kernel's packed varint pairs against a plain zigzag-LEB128 encoder:

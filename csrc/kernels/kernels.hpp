@@ -217,7 +217,8 @@ void launch_decode(int M, int K, int L, uint32_t m, int value_bytes, const uint8
 // Fused clerk decode + combine over rows R (clerks) x P participants, message
 // j = r * P + p. pre [M][S] = exclusive sub-chunk terminator ranks (segscan of
 // sub_cnt), totals [M]; tile_sub [M][T+1] scratch (T = ceil(L / kSumTile));
-// part [G][R][L] scratch slabs (G = ceil(P / Pg); needs Pg * (m - 1) < 2^32);
+// part [G][R][L] scratch slabs (G = ceil(P / Pg); needs Pg * (m - 1) < 2^32 unless
+// decode_sum_wide(m): then two words per entry and no bound on Pg);
 // out [R][L] = sum_p values mod m.
 void launch_locate_tiles(int M, int S, int L, const uint32_t* pre, const uint32_t* totals,
                          uint32_t* tile_sub, hipStream_t s);
@@ -225,6 +226,9 @@ void launch_locate_tiles(int M, int S, int L, const uint32_t* pre, const uint32_
 // kernel (sums of zigzag codes, no per-element decode) runs first and the
 // generic one only if a stream is not canonical (long or negative varints);
 // needs Pg * 16383 < 2^32 as well.
+// Moduli above 2^27 (past the lean kernels' four-byte codes) are summed in 64-bit
+// accumulators: `part` then holds two words per sum, and a group may be any size.
+inline bool decode_sum_wide(uint32_t m) { return m > (1u << 27); }
 void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* pt, uint64_t stride,
                        const uint32_t* pt_len, int S, const uint32_t* pre, const uint32_t* tile_sub,
                        uint32_t* part, uint32_t* out, int64_t* acc, uint32_t* err, uint32_t* redo,

@@ -33,8 +33,24 @@ inline ModParams make_mod_params(uint32_t m) {
   return p;
 }
 
+// High halves of the products: the device instructions, or plain C for the host runs
+// of the device algorithms (host_emul.cpp).
+SDA_DEV uint32_t mulhi32(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umulhi(a, b);
+#else
+  return (uint32_t)(((uint64_t)a * b) >> 32);
+#endif
+}
+SDA_DEV uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
 SDA_DEV uint32_t mod32(uint32_t w, const ModParams& P) {
-  uint32_t q = __umulhi(w, P.mu32);
+  uint32_t q = mulhi32(w, P.mu32);
   uint32_t r = w - q * P.m;
   return r >= P.m ? r - P.m : r;
 }
@@ -93,7 +109,7 @@ SDA_DEV uint32_t modf64d(double vd, const ModF64& P) {
 }
 SDA_DEV uint32_t modf64(uint64_t v, const ModF64& P) { return modf64d((double)(int64_t)v, P); }
 SDA_DEV uint32_t mod64(uint64_t v, const ModParams& P) {
-  uint64_t q = __umul64hi(v, P.mu64);
+  uint64_t q = mulhi64(v, P.mu64);
   uint64_t r = v - q * (uint64_t)P.m;  // q >= floor(v/m) - 2
   r = r >= P.m ? r - P.m : r;
   r = r >= P.m ? r - P.m : r;

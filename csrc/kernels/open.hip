@@ -11,6 +11,8 @@
 // the lanes rank their terminators with a block scan and each lane decodes the
 // varints ending in its 64 bytes, reading at most 9 bytes back (a 16-byte LDS
 // prefix of the previous chunk covers varints straddling the boundary).
+#include <type_traits>
+
 #include "block_utils.hpp"
 #include "decode_core.hpp"
 #include "device_crypto.hpp"
@@ -56,8 +58,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   const int64_t p0 = kC - 32 + 64 * tid;  // message position of this lane's first byte
   uint32_t w[16];
   load_lane_bytes(w, gmsg, p0, end);
-  uint32_t wave_prev = 0;
+  uint32_t wave_prev = 0, wave_prev2 = 0;  // the 8 bytes before a wave's first lane
   if ((tid & 63) == 0 && p0 - 4 >= 0 && p0 - 4 < end) wave_prev = *reinterpret_cast<const uint32_t*>(gmsg + p0 - 4);
+  if ((tid & 63) == 0 && p0 - 8 >= 0 && p0 - 8 < end) wave_prev2 = *reinterpret_cast<const uint32_t*>(gmsg + p0 - 8);
   const int lo = (int)max((int64_t)0, start - p0);
   const int hi = (int)min((int64_t)64, end - p0);
   const uint64_t traw = term_mask64(w);
@@ -65,8 +68,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   uint32_t total;
   const uint32_t local = block_excl_scan((uint32_t)__popcll(tmask), scratch, &total);  // syncs
   const uint32_t prev_word = wave_shift_up1(w[15], wave_prev);  // lane 0: from global
+  const uint32_t prev_word2 = wave_shift_up1(w[14], wave_prev2);
   StageSink<VT> sink{outb, (uint32_t)(kChunkBytes + 2 * (tid & 63))};
-  bool bad = decode_lane<sizeof(VT) == 2>(w, prev_word, tmask, traw, local, mp, gmsg, p0, sink);
+  bool bad = decode_lane<sizeof(VT) == 2>(w, prev_word2, prev_word, tmask, traw, local, mp, gmsg, p0, sink);
   // a message must end on a terminator
   if (hi > lo && p0 + hi == (int64_t)N && (gmsg[N - 1] & 0x80)) bad = true;
   __syncthreads();
@@ -108,6 +112,20 @@ struct AddSink {
   SDA_DEV void put_rank(uint32_t rank, uint32_t v) { atomicAdd(acc + (rank + off), v); }
 };
 
+// The same into 64-bit accumulators (ds_add_u64): moduli above 2^27, whose values a u32
+// accumulator can add up only a handful of (two at 2^31 - 1: 500 slabs of a million
+// sums each to write and add again for 1000 participants; that was 63 % of such a round).
+struct AddSink64 {
+  static constexpr bool kAdditive = true;
+  unsigned long long* acc;
+  uint32_t off;
+  SDA_DEV void put(uint32_t local, uint32_t v, uint32_t term) {
+    atomicAdd(acc + (local + off), (unsigned long long)(v & (0u - term)));
+  }
+  SDA_DEV void put_masked(uint32_t local, uint32_t v) { atomicAdd(acc + (local + off), (unsigned long long)v); }
+  SDA_DEV void put_rank(uint32_t rank, uint32_t v) { atomicAdd(acc + (rank + off), (unsigned long long)v); }
+};
+
 __global__ void __launch_bounds__(kBlock)
     k_locate_tiles(int S, int T, const uint32_t* __restrict__ pre,
                    const uint32_t* __restrict__ totals, uint32_t* __restrict__ tile_sub) {
@@ -130,12 +148,12 @@ __global__ void __launch_bounds__(kBlock)
 // passes -- 64 lanes x 64 bytes, ranks by a wave scan -- so no block barrier
 // sits between a pass's loads and the next: 16 independent waves per CU keep
 // their loads in flight. The waves share the tile accumulator through ds_add.
-template <bool kFast16, typename Sink>
-SDA_DEV void decode_sum_body(uint32_t* acc, uint32_t (*info)[4], int L, int P, int Pg,
+template <bool kFast16, typename Sink, typename AccT>
+SDA_DEV void decode_sum_body(AccT* acc, uint32_t (*info)[4], int L, int P, int Pg,
                              const ModParams& mp, const uint8_t* __restrict__ pt, uint64_t stride,
                              const uint32_t* __restrict__ pt_len, int S,
                              const uint32_t* __restrict__ pre, const uint32_t* __restrict__ tile_sub,
-                             uint32_t* __restrict__ part, uint32_t* err) {
+                             AccT* __restrict__ part, uint32_t* err) {
   constexpr int kWaveBytes = 64 * 64;
   const int t = blockIdx.x, r = blockIdx.y, g = blockIdx.z, R = gridDim.y;
   const int T = gridDim.x;
@@ -170,8 +188,9 @@ SDA_DEV void decode_sum_body(uint32_t* acc, uint32_t (*info)[4], int L, int P, i
         const int64_t p0 = c0 + 64 * lane;
         uint32_t w[16];
         load_lane_bytes(w, gmsg, p0, qe);
-        uint32_t wave_prev = 0;
+        uint32_t wave_prev = 0, wave_prev2 = 0;
         if (lane == 0 && p0 - 4 >= 0 && p0 - 4 < N) wave_prev = *reinterpret_cast<const uint32_t*>(gmsg + p0 - 4);
+        if (lane == 0 && p0 - 8 >= 0 && p0 - 8 < N) wave_prev2 = *reinterpret_cast<const uint32_t*>(gmsg + p0 - 8);
         const int lo = (int)max((int64_t)0, qs - p0);
         const int hi = (int)min((int64_t)64, qe - p0);
         const uint64_t traw = term_mask64(w);
@@ -180,33 +199,35 @@ SDA_DEV void decode_sum_body(uint32_t* acc, uint32_t (*info)[4], int L, int P, i
         const uint32_t incl = wave_incl_scan(c);
         const uint32_t total = wave_read_lane(incl, 63);
         const uint32_t prev_word = wave_shift_up1(w[15], wave_prev);  // lane 0: from global
+        const uint32_t prev_word2 = wave_shift_up1(w[14], wave_prev2);
         Sink sink{acc, rank + kSumMargin - E0};
-        bad |= decode_lane<kFast16>(w, prev_word, tmask, traw, incl - c, mp, gmsg, p0, sink);
+        bad |= decode_lane<kFast16>(w, prev_word2, prev_word, tmask, traw, incl - c, mp, gmsg, p0, sink);
         if (hi > lo && p0 + hi == N && (gmsg[N - 1] & 0x80)) bad = true;
         rank += total;
       }
     }
   }
   __syncthreads();
-  uint32_t* out = part + ((size_t)g * R + r) * L + E0;
+  AccT* out = part + ((size_t)g * R + r) * L + E0;
   for (uint32_t i = tid; i < W; i += kBlock) out[i] = acc[kSumMargin + i];
   if (bad) atomicOr(err, kErrMalformed);
 }
 
 // No occupancy hint: the unrolled decode paths need ~200 VGPRs (2 waves per
 // SIMD); squeezing them into 128 or 168 spilled and measured slower.
-template <bool kFast16>
+template <bool kFast16, bool kWide>
 __global__ void __launch_bounds__(kBlock)
     k_decode_sum(int L, int P, int Pg, ModParams mp, const uint8_t* __restrict__ pt,
                  uint64_t stride, const uint32_t* __restrict__ pt_len, int S,
                  const uint32_t* __restrict__ pre, const uint32_t* __restrict__ tile_sub,
                  uint32_t* __restrict__ part, uint32_t* err, const uint32_t* gate) {
-  __shared__ uint32_t acc[kSumAcc];
+  using AccT = std::conditional_t<kWide, unsigned long long, uint32_t>;
+  __shared__ AccT acc[kSumAcc];
   __shared__ uint32_t info[kBlock][4];
   // behind the lean kernel: only if it met a stream it does not handle
   if (gate != nullptr && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
-  decode_sum_body<kFast16, AddSink>(acc, info, L, P, Pg, mp, pt, stride, pt_len, S, pre, tile_sub,
-                                    part, err);
+  decode_sum_body<kFast16, std::conditional_t<kWide, AddSink64, AddSink>, AccT>(
+      acc, info, L, P, Pg, mp, pt, stride, pt_len, S, pre, tile_sub, reinterpret_cast<AccT*>(part), err);
 }
 
 // ---------------------------------------- clerk decode + combine, lean form
@@ -529,6 +550,20 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+// The same over 64-bit slabs (k_decode_sum<.., true>: sums of canonical values).
+__global__ void __launch_bounds__(kBlock)
+    k_sum_slabs64(int G, int64_t X, ModParams mp, const unsigned long long* __restrict__ part,
+                  uint32_t* __restrict__ out, int64_t* __restrict__ acc) {
+  const int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (x >= X) return;
+  // every slab's sum is below P 2^32; reduced one by one, the total of residues below G 2^32
+  uint64_t a = 0;
+  for (int g = 0; g < G; ++g) a += mod64(part[(int64_t)g * X + x], mp);
+  const uint32_t r = mod64(a, mp);
+  if (acc != nullptr) acc[x] += r;
+  else out[x] = r;
+}
+
 template <typename VT, typename ACC>
 __global__ void __launch_bounds__(kBlock)
     k_colsum(int R, int L, ModParams mp, const VT* __restrict__ vals, uint32_t* __restrict__ out) {
@@ -648,13 +683,21 @@ void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* p
                        tile_sub, part, redo, err, three ? 1 : 0);
   }
   const uint32_t* gate = lean ? redo : nullptr;
+  const int64_t X = (int64_t)R * L;
+  if (decode_sum_wide(m)) {
+    // values a u32 accumulator could add up only a few of: 64-bit accumulators and slabs
+    hipLaunchKernelGGL((k_decode_sum<false, true>), grid, dim3(kBlock), 0, s, L, P, Pg, mp, pt, stride,
+                       pt_len, S, pre, tile_sub, part, err, gate);
+    hipLaunchKernelGGL(k_sum_slabs64, dim3((unsigned)((X + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, G, X, mp,
+                       reinterpret_cast<const unsigned long long*>(part), out, acc);
+    return;
+  }
   if (m < 65536u)
-    hipLaunchKernelGGL(k_decode_sum<true>, grid, dim3(kBlock), 0, s, L, P, Pg, mp, pt, stride,
+    hipLaunchKernelGGL((k_decode_sum<true, false>), grid, dim3(kBlock), 0, s, L, P, Pg, mp, pt, stride,
                        pt_len, S, pre, tile_sub, part, err, gate);
   else
-    hipLaunchKernelGGL(k_decode_sum<false>, grid, dim3(kBlock), 0, s, L, P, Pg, mp, pt, stride,
+    hipLaunchKernelGGL((k_decode_sum<false, false>), grid, dim3(kBlock), 0, s, L, P, Pg, mp, pt, stride,
                        pt_len, S, pre, tile_sub, part, err, gate);
-  const int64_t X = (int64_t)R * L;
   const int64_t threads = (X + 3) / 4;
   hipLaunchKernelGGL(k_sum_slabs, dim3((unsigned)((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                      G, X, mp, part, out, gate, acc);

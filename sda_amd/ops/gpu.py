@@ -417,17 +417,22 @@ def locate_tiles(pre: torch.Tensor, totals: torch.Tensor, L: int, tile_sub: torc
     _gpu().locate_tiles(M, S, L, _ptr(pre), _ptr(totals), _ptr(tile_sub), _stream())
 
 
+def decode_sum_wide(modulus: int) -> bool:
+    """Moduli above 2^27 are summed in 64-bit accumulators (two words per slab entry)."""
+    return modulus > 1 << 27
+
+
 def decode_sum_group_limit(modulus: int) -> int:
-    """Most participants one decode-sum accumulator (u32) may add up: sums of
-    canonical values, or on the lean path sums of zigzag codes of up to 14 bits
-    (m <= 2^13: two-byte varints), 21 bits (2 (m - 1) < 2^21: three bytes) or 28 bits
-    (m <= 2^27: four bytes)."""
+    """Most participants one decode-sum accumulator may add up. u32 accumulators hold
+    sums of zigzag codes of up to 14 bits (m <= 2^13: two-byte varints), 21 bits
+    (2 (m - 1) < 2^21: three bytes) or 28 bits (m <= 2^27: four bytes); above that the
+    accumulators are 64 bits wide and any group fits."""
+    if decode_sum_wide(modulus):
+        return 1 << 30
     if modulus <= 8192:
         per = 16383
-    elif modulus <= 1 << 27:  # a longer code than the field's raises the fallback
+    else:  # a longer code than the field's raises the fallback
         per = (1 << 21) - 1 if 2 * (modulus - 1) < 1 << 21 else (1 << 28) - 1
-    else:
-        per = modulus - 1
     return max(1, (2 ** 32 - 1) // max(1, per))
 
 
@@ -442,7 +447,7 @@ def decode_sum(rows: int, P: int, Pg: int, L: int, modulus: int, pt, stride, pt_
     if modulus <= 0:
         raise ValueError("decode_sum needs a modulus")
     if Pg < 1 or Pg > decode_sum_group_limit(modulus):
-        raise ValueError("decode_sum: the group's sums must fit the u32 accumulators")
+        raise ValueError("decode_sum: the group's sums must fit the accumulators")
     if redo is not None:
         _check(redo, "redo", torch.int32, numel=1)
     groups = (P + Pg - 1) // Pg
@@ -450,7 +455,7 @@ def decode_sum(rows: int, P: int, Pg: int, L: int, modulus: int, pt, stride, pt_
     _check(pt_len, "pt_len", torch.int32, numel=M)
     _check(pre, "pre", torch.int32, numel=M * S)
     _check(tile_sub, "tile_sub", torch.int32, numel=M * (sum_tiles(L) + 1))
-    _check(part, "part", torch.int32, numel=groups * rows * L)
+    _check(part, "part", torch.int32, numel=groups * rows * L * (2 if decode_sum_wide(modulus) else 1))
     if acc is not None:
         _check(acc, "acc", torch.int64, numel=rows * L)
     else:

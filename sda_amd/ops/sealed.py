@@ -332,7 +332,8 @@ def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
     tile_sub = torch.empty(M, T + 1, dtype=torch.int32, device=dev)
     G.locate_tiles(pre, totals, L, tile_sub)
     Pg = decode_group_size(P, T * rows, G.decode_sum_group_limit(m))
-    part = torch.empty(-(-P // Pg), rows, L, dtype=torch.int32, device=dev)
+    part = torch.empty(-(-P // Pg) * (2 if G.decode_sum_wide(m) else 1), rows, L, dtype=torch.int32,
+                       device=dev)
     redo = torch.zeros(1, dtype=torch.int32, device=dev)
     G.decode_sum(rows, P, Pg, L, m, arena.ct, arena.stride, arena.pt_len, pre, tile_sub, part,
                  out, err, redo, acc=acc)

@@ -166,7 +166,7 @@ def fixed_bytes(spec: AggregationSpec, streamed: bool) -> int:
     tile each), combined shares, the result boxes, the output; running int64 sums
     when streamed."""
     n, m, D, B = spec.n_clerks, spec.field_modulus, spec.dimension, spec.batches
-    slabs = 10_000 * SUM_TILE * 4 + n * B * 4
+    slabs = 10_000 * SUM_TILE * (8 if m > 2 ** 27 else 4) + n * B * 4   # 64-bit sums above 2^27
     b = slabs + n * B * 4 + n * _box_bytes(B, m, True) + 2 * D * 4
     if spec.masking.has_mask():
         b += 10_000 * SUM_TILE * 4 + D * 4 + D * 8   # mask slabs / sums / ChaCha fix-up words

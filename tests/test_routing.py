@@ -151,3 +151,7 @@ def test_decode_group_size_rule():
     assert decode_sum_group_limit(433) == (2 ** 32 - 1) // 16383
     assert decode_sum_group_limit(746497) == (2 ** 32 - 1) // (2 ** 21 - 1)
     assert decode_sum_group_limit(5038849) == (2 ** 32 - 1) // (2 ** 28 - 1)
+    # above 2^27 the accumulators are 64 bits wide: the group size is the block-count rule's
+    assert decode_sum_group_limit(2 ** 31 - 1) >= 10000
+    assert decode_group_size(1000, 489, decode_sum_group_limit(2 ** 31 - 1)) == \
+        decode_group_size(1000, 489, lim)
