@@ -76,6 +76,21 @@ def test_modgemm_transposed_truncated_store(cuda, panel, p):
     assert torch.equal(out.cpu().to(torch.int64), ref)
 
 
+@pytest.mark.parametrize("p", [433, 746497, 5038849, (1 << 27) - 39])
+@pytest.mark.parametrize("R,N", [(255, 40), (300, 130), (64, 64), (5, 1), (1000, 257)])
+def test_limbs_t_is_limbs_of_the_transpose(cuda, p, R, N):
+    """The tiled transpose-to-limbs kernel against the elementwise limb split (every limb
+    scheme; ragged row and column tiles)."""
+    from sda_amd.ops import gpu as G
+
+    g = torch.Generator().manual_seed(R * N)
+    Y = torch.randint(0, p, (R, N), generator=g, dtype=torch.int64).to(torch.int32).cuda()
+    Kp = G.padded_k(R)
+    got = G.limbs_t(Y, Kp, p)
+    ref = G.limbs_of(Y.T.contiguous(), Kp, p)
+    assert torch.equal(got[:, 0], ref)
+
+
 @pytest.mark.parametrize("prime,dtype", [(746497, torch.int32), (5038849, torch.int32),
                                          (433, torch.int16), (60013, torch.int16)])
 @pytest.mark.parametrize("M,N,Z,panel", [(37, 45, 2, 0), (70, 4096 + 300, 3, 0), (9, 9000, 1, 0),
