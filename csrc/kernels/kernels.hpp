@@ -237,6 +237,9 @@ void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* p
 void set_decode_lean(int mode);
 // lean decode-sum accumulator layout: -1 padded rows by modulus (default), 0 never, 1 always
 void set_decode_swz(int mode);
+// lean decode-sum of three- and four-byte fields: 1 walks values (one LDS add per value),
+// 0 adds byte by byte like the short-code kernel, -1 (default) the former for three-byte fields
+void set_decode_long(int mode);
 // Column sums mod m: out[g][l] = sum_r vals[g][r][l] mod m.
 void launch_colsum(int G, int R, int L, uint32_t m, int value_bytes, const void* vals,
                    uint32_t* out, hipStream_t s);

@@ -279,9 +279,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     k_decode_sum_z(int L, int P, int Pg, const uint8_t* __restrict__ pt, uint64_t stride,
                    const uint32_t* __restrict__ pt_len, int S, const uint32_t* __restrict__ pre,
                    const uint32_t* __restrict__ tile_sub, uint32_t* __restrict__ part,
-                   uint32_t* redo, uint32_t* err, int three) {
-  // three (kMaxBytes = 4 only): the field's codes have at most three bytes, a fourth
-  // raises `redo` (the caller sized the participant groups for 21-bit codes)
+                   uint32_t* redo, uint32_t* err) {
+  // kMaxBytes = 3: the field's codes have at most three bytes, a fourth raises `redo`
+  // (the caller sized the participant groups for 21-bit codes)
+  constexpr bool three = kMaxBytes == 3;
   constexpr int kWaveBytes = 64 * 64;
   // pad stride: every 32 words for two-byte codes (ranks 32 apart -> 33), every 16 for
   // the long ones (21.33 / 16 apart -> 22.67 / 17: odd and even banks alike)
@@ -383,10 +384,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
             const uint64_t craw = ~term_mask64(w);
             if (lo > 0) K |= craw & (1ull << (lo - 1));
             uint64_t run = craw & (1ull << (hi - 1));  // continuation bytes at the end: the next lane's
-            if constexpr (kMaxBytes > 2) {
-              run |= (run >> 1) & craw;
-              run |= (run >> 1) & craw;
-            }
+            if constexpr (kMaxBytes > 2) run |= (run >> 1) & craw;
+            if constexpr (kMaxBytes > 3) run |= (run >> 1) & craw;
             K &= ~run;
           }
           if (lo > 0 || hi <= lo) pm1 = 0;  // the byte before this lane is not its to add
@@ -402,12 +401,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
           // a continuation byte in the last position belongs to the next lane's element
           if constexpr (kMaxBytes <= 2) {
             w[15] &= ~((uint32_t)((int32_t)w[15] >> 31) & 0xff000000u);
-          } else {  // ... the run of up to three of them
+          } else {  // ... the run of up to three (two) of them
             const uint32_t x15 = w[15];
             const uint32_t t3 = (uint32_t)((int32_t)x15 >> 31);
             const uint32_t t2 = t3 & (uint32_t)((int32_t)(x15 << 8) >> 31);
-            const uint32_t t1 = t2 & (uint32_t)((int32_t)(x15 << 16) >> 31);
-            w[15] = x15 & ~((t3 & 0xff000000u) | (t2 & 0x00ff0000u) | (t1 & 0x0000ff00u));
+            uint32_t drop = (t3 & 0xff000000u) | (t2 & 0x00ff0000u);
+            if constexpr (kMaxBytes > 3) drop |= t2 & (uint32_t)((int32_t)(x15 << 16) >> 31) & 0x0000ff00u;
+            w[15] = x15 & ~drop;
           }
         }
         uint32_t c = 0;
@@ -431,8 +431,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
             const uint32_t x = w[q];
             const uint32_t c1 = __builtin_amdgcn_alignbyte(x, wp, 3) & 0x80808080u;
             const uint32_t c2 = c1 & __builtin_amdgcn_alignbyte(x, wp, 2);
-            const uint32_t c3 = c2 & __builtin_amdgcn_alignbyte(x, wp, 1);
-            bad |= x & (three ? c2 : c3);                       // one continuation byte too many in a row
+            if constexpr (three) {
+              bad |= x & c2;                                    // one continuation byte too many in a row
+            } else {
+              bad |= x & c2 & __builtin_amdgcn_alignbyte(x, wp, 1);
+            }
             bad |= x & 0x01010101u & ~(c1 >> 7);                // odd first byte: a negative value
             c += (uint32_t)__popc(tw[q]);
             wp = x;
@@ -441,7 +444,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
           // it out): b3 is the byte before, then b2, b1; its first byte has shift 0
           const uint32_t b1 = (pm1 >> 8) & 0xffu, b2 = (pm1 >> 16) & 0xffu, b3 = pm1 >> 24;
           const bool t3 = b3 & 0x80u, t2 = t3 && (b2 & 0x80u), t1 = t2 && (b1 & 0x80u);
-          lead = t1 ? ((b1 & 0x7fu) | ((b2 & 0x7fu) << 7) | ((b3 & 0x7fu) << 14))
+          // (three continuation bytes before the lane: a four-byte code, flagged below when
+          // the field has none; the previous lane then kept the first of them)
+          lead = t1 && !three ? ((b1 & 0x7fu) | ((b2 & 0x7fu) << 7) | ((b3 & 0x7fu) << 14))
                : t2 ? ((b2 & 0x7fu) | ((b3 & 0x7fu) << 7))
                : t3 ? (b3 & 0x7fu) : 0u;
           bad |= lead & 1u;                                     // odd first byte of that run
@@ -462,8 +467,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
           uint32_t pc = (__builtin_amdgcn_alignbyte(x, wp, 3) & 0x80808080u) >> 7;
           if constexpr (kMaxBytes > 2) {
             const uint32_t c2 = pc & (__builtin_amdgcn_alignbyte(x, wp, 2) >> 7);
-            const uint32_t c3 = c2 & (__builtin_amdgcn_alignbyte(x, wp, 1) >> 7);
-            pc += c2 + c3;
+            if constexpr (kMaxBytes > 3) pc += c2 & (__builtin_amdgcn_alignbyte(x, wp, 1) >> 7);
+            pc += c2;
           }
           // (opaque steps: left to itself the compiler folds these shift-adds into
           // v_mul_lo_u32, a quarter-rate instruction, and the byte fields below
@@ -498,6 +503,191 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     out[i] = acc[kSwz ? x + (x >> kPadShift) : x];
   }
   if (bad) atomicOr(redo, 1u);
+  if (malformed) atomicOr(err, kErrMalformed);
+}
+
+// ------------------------------- clerk decode + combine, lean form for long codes
+// Fields whose codes are mostly three or four bytes long (the large packed-Shamir
+// primes) spend the byte-wise kernel above badly: three or four LDS adds and ~60 VALU
+// instructions per value. Here a wave stages its 4 KiB pass in LDS and every lane walks
+// its own terminators: the four bytes ending at a terminator come back as one unaligned
+// LDS read whatever lane they started in, the run of continuation bits in front of the
+// terminator (0..3) says how many of the four 7-bit groups belong to the code, and the
+// code goes to its rank in one add: ~28 VALU instructions and two LDS accesses per
+// value. A value belongs to the lane that holds its terminator, so there is no
+// hand-over of leading or trailing bytes between lanes. Codes longer than kMaxBytes
+// (any run of kMaxBytes continuation bytes, inside a lane or across two) and odd codes
+// (negative values) raise `redo` as above.
+template <int kMaxBytes, bool kSwz>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
+    k_decode_sum_v(int L, int P, int Pg, const uint8_t* __restrict__ pt, uint64_t stride,
+                   const uint32_t* __restrict__ pt_len, int S, const uint32_t* __restrict__ pre,
+                   const uint32_t* __restrict__ tile_sub, uint32_t* __restrict__ part,
+                   uint32_t* redo, uint32_t* err) {
+  static_assert(kMaxBytes == 3 || kMaxBytes == 4, "codes of three or four bytes");
+  constexpr int kWaveBytes = 64 * 64;
+  constexpr int kPadShift = 5;  // one pad word per 32 ranks
+  constexpr int kAccWords = kSwz ? kSumAcc + (kSumAcc >> kPadShift) + 1 : kSumAcc;
+  constexpr int kStageWords = kWaveBytes / 4 + 4;  // the pass from word 4 (16-byte aligned), the 4 bytes before it in word 3
+  __shared__ uint32_t acc[kAccWords];
+  constexpr int kBatch = 128;  // messages whose tile descriptors are staged at a time
+  __shared__ uint32_t info[kBatch][4];
+  __shared__ __attribute__((aligned(16))) uint32_t stage[kWaves][kStageWords];
+  auto add = [&](uint32_t byte_off, uint32_t v) {
+    lds_add(acc, kSwz ? byte_off + ((byte_off >> (kPadShift + 2)) << 2) : byte_off, v);
+  };
+  const int t = blockIdx.x, r = blockIdx.y, g = blockIdx.z, R = gridDim.y;
+  const int T = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t E0 = (uint32_t)t * kSumTile;
+  const uint32_t W = min((uint32_t)kSumTile, (uint32_t)L - E0);
+  for (int i = tid; i < kAccWords; i += kBlock) acc[i] = 0;
+  // this wave's staging area
+  uint8_t* const sbytes = reinterpret_cast<uint8_t*>(&stage[wave][4]);
+  const int pbeg = g * Pg, pend = min(P, pbeg + Pg);
+  uint32_t bad = 0;
+  bool malformed = false;
+  for (int b0 = pbeg; b0 < pend; b0 += kBatch) {
+    const int cnt = min(kBatch, pend - b0);
+    __syncthreads();  // previous batch's info reads done (and acc zeroed)
+    if (tid < cnt) {
+      const size_t j = (size_t)r * P + b0 + tid;
+      const uint32_t s0 = tile_sub[j * (T + 1) + t];
+      info[tid][0] = s0;
+      info[tid][1] = tile_sub[j * (T + 1) + t + 1];
+      info[tid][2] = s0 < (uint32_t)S ? pre[j * S + s0] : 0u;
+      info[tid][3] = pt_len[j];
+    }
+    __syncthreads();
+    // work items (message, 4 KiB pass) as in k_decode_sum_z: the next item's bytes are in
+    // flight while the current one is processed
+    int ni = wave;
+    const uint8_t* n_gmsg = nullptr;
+    int64_t n_c0 = 0, n_qs = 0, n_qe = 0, n_N = 0;
+    uint32_t n_rank = 0;
+    bool n_first = false, n_valid = false;
+    auto open_next = [&]() {
+      if (n_valid && n_c0 + kWaveBytes < n_qe) {
+        n_c0 += kWaveBytes;
+        n_first = false;
+        return;
+      }
+      n_valid = false;
+      while (ni < cnt) {
+        const int i = ni;
+        ni += kWaves;
+        const uint32_t s0 = info[i][0];
+        if (s0 >= (uint32_t)S) continue;  // fewer elements than the tile start: flagged by the totals
+        const uint32_t s1 = min(info[i][1], (uint32_t)S - 1);
+        n_N = info[i][3];
+        n_gmsg = pt + ((size_t)r * P + b0 + i) * stride + 48;
+        n_qs = max((int64_t)0, (int64_t)s0 * kSubBytes - 32);
+        n_qe = min(n_N, ((int64_t)s1 + 1) * kSubBytes - 32);
+        n_c0 = (int64_t)s0 * kSubBytes - 32;
+        n_rank = info[i][2];
+        n_first = true;
+        n_valid = n_c0 < n_qe;
+        if (n_valid) return;
+      }
+    };
+    uint32_t wn[16], pn = 0;  // the next item's bytes, and the 4 bytes before lane 0's
+    auto fetch_next = [&]() {
+      const int64_t p0 = n_c0 + 64 * lane;
+      load_lane_bytes(wn, n_gmsg, p0, n_qe);
+      pn = 0;
+      if (lane == 0 && p0 - 4 >= 0 && p0 - 4 < n_N) pn = *reinterpret_cast<const uint32_t*>(n_gmsg + p0 - 4);
+    };
+    open_next();
+    if (n_valid) fetch_next();
+    uint32_t rank = 0;
+    while (n_valid) {
+      const uint8_t* gmsg = n_gmsg;
+      const int64_t c0 = n_c0, qs = n_qs, qe = n_qe, N = n_N;
+      if (n_first) rank = n_rank;
+      uint32_t w[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) w[q] = wn[q];
+      const uint32_t wave_prev = pn;
+      open_next();
+      if (n_valid) fetch_next();
+      const int64_t p0 = c0 + 64 * lane;
+      const int lo = (int)max((int64_t)0, qs - p0);
+      const int hi = (int)min((int64_t)64, qe - p0);
+      if (hi > lo && p0 + hi == N && (gmsg[N - 1] & 0x80)) malformed = true;  // must end on a terminator
+      // the pass into LDS (the previous item's reads were issued before these writes)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<uint4*>(sbytes + 64 * lane + 16 * q) =
+            make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+      if (lane == 0) stage[wave][3] = wave_prev;
+      const uint64_t traw = term_mask64(w);
+      const uint64_t tmask = traw & byte_range_mask(lo, hi);
+      // too long a code: kMaxBytes continuation bytes in a row, within the lane ...
+      {
+        // (bytes from `hi` on are the next range's or past the message: taken as terminators)
+        const uint64_t tv = traw | ~byte_range_mask(0, hi);
+        const uint64_t craw = ~tv;
+        uint64_t runs = craw & (craw >> 1) & (craw >> 2);
+        if constexpr (kMaxBytes > 3) runs &= craw >> 3;
+        // ... or across the lane's start: those at the end of the lane before + those here
+        const uint32_t head = tv ? (uint32_t)__builtin_ctzll(tv) : 64u;
+        const uint32_t tail = tv ? (uint32_t)__builtin_clzll(tv) : 64u;
+        const uint32_t hist = ~wave_prev & 0x80808080u;  // lane 0: the four bytes before the pass
+        const uint32_t tail0 = hist ? (uint32_t)__builtin_clz(hist) >> 3 : 4u;
+        const uint32_t before = wave_shift_up1(tail, tail0);
+        bad |= (runs != 0 ? 0x80u : 0u) | (before + head >= (uint32_t)kMaxBytes ? 0x40u : 0u);
+      }
+      const uint32_t c = (uint32_t)__popcll(tmask);
+      const uint32_t incl = wave_incl_scan(c);
+      const uint32_t total = wave_read_lane(incl, 63);
+      uint32_t a4 = 4u * (rank + kSumMargin - E0 + (incl - c));  // byte offset of the lane's first rank
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // the lane's terminators, low half of its bytes then high half; the window of the
+      // next terminator is requested before the current one is worked on
+      const uint8_t* mine = sbytes + 64 * lane - 3;
+      auto window = [&](int p) {  // bytes p - 3 .. p of the lane: the terminator on top
+        uint32_t win;
+        __builtin_memcpy(&win, mine + p, 4);
+        return win;
+      };
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        uint32_t tm = half ? (uint32_t)(tmask >> 32) : (uint32_t)tmask;
+        uint32_t next = tm != 0 ? window(__builtin_ctz(tm) + 32 * half) : 0u;
+        while (__builtin_amdgcn_ballot_w64(tm != 0) != 0) {
+          if (tm != 0) {
+            const uint32_t win = next;
+            tm &= tm - 1;
+            if (tm != 0) next = window(__builtin_ctz(tm) + 32 * half);
+            const uint32_t m7 = win >> 7;
+            const uint32_t c2 = (m7 >> 16) & 1u;   // byte p - 1 continues
+            const uint32_t c1 = (m7 >> 8) & c2;    // ... and p - 2
+            const uint32_t c0 = m7 & c1;           // ... and p - 3
+            const uint32_t rl = c2 + c1 + c0;
+            const uint32_t g7 = win & 0x7f7f7f7fu;
+            const uint32_t x = (g7 & 0x007f007fu) | ((g7 & 0x7f007f00u) >> 1);
+            const uint32_t full = (x & 0x3fffu) | ((x >> 2) & 0x0fffc000u);
+            const uint32_t z = full >> (21u - 7u * rl);
+            bad |= z & 1u;  // odd: a negative value
+            add(a4, z);
+            a4 += 4u;
+          }
+        }
+      }
+      rank += total;
+    }
+  }
+  __syncthreads();
+  uint32_t* out = part + ((size_t)g * R + r) * L + E0;
+  for (uint32_t i = tid; i < W; i += kBlock) {
+    const uint32_t x = kSumMargin + i;
+    out[i] = acc[kSwz ? x + (x >> kPadShift) : x];
+  }
+  if (bad) atomicOr(redo, bad);  // 0x80 / 0x40: a code too long (inside a lane / across two), 1: an odd code
   if (malformed) atomicOr(err, kErrMalformed);
 }
 
@@ -629,6 +819,8 @@ __global__ void k_sub_mod(int D, uint32_t m, const uint32_t* __restrict__ a,
 
 static int g_decode_lean = 1;
 void set_decode_lean(int mode) { g_decode_lean = mode; }
+static int g_decode_long = -1;  // long-code lean decode: -1 by field, 1 value-wise (k_decode_sum_v), 0 byte-wise
+void set_decode_long(int mode) { g_decode_long = mode; }
 static int g_decode_swz = -1;  // padded accumulator rows: -1 by modulus, 0 never, 1 always
 void set_decode_swz(int mode) { g_decode_swz = mode; }
 
@@ -676,11 +868,21 @@ void launch_decode_sum(int R, int P, int Pg, int L, uint32_t m, const uint8_t* p
   if (lean && m <= 8192u) {
     auto kern = swz ? k_decode_sum_z<2, true> : k_decode_sum_z<2, false>;
     hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S, pre,
-                       tile_sub, part, redo, err, 0);
+                       tile_sub, part, redo, err);
   } else if (lean) {  // canonical codes 2 (m - 1) below 2^21 have at most three bytes
-    auto kern = swz ? k_decode_sum_z<4, true> : k_decode_sum_z<4, false>;
+    // value-wise kernel or byte-wise one. Measured: three-byte codes, 1000 participants a
+    // row: 18.0 against 22.3 ms (728 rows); four-byte codes, 16 participants a row: 8.2
+    // against 5.6 ms (19,682 rows: the value-wise kernel's larger LDS footprint -- three
+    // workgroups a CU instead of four -- and per-workgroup set-up weigh more than its
+    // fewer LDS adds). g_decode_long: -1 by that rule (default), 0 byte-wise, 1 value-wise.
+    const bool by_value = g_decode_long < 0 ? three : g_decode_long != 0;
+    auto kern = by_value
+                    ? (three ? (swz ? k_decode_sum_v<3, true> : k_decode_sum_v<3, false>)
+                             : (swz ? k_decode_sum_v<4, true> : k_decode_sum_v<4, false>))
+                    : (three ? (swz ? k_decode_sum_z<3, true> : k_decode_sum_z<3, false>)
+                             : (swz ? k_decode_sum_z<4, true> : k_decode_sum_z<4, false>));
     hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, P, Pg, pt, stride, pt_len, S, pre,
-                       tile_sub, part, redo, err, three ? 1 : 0);
+                       tile_sub, part, redo, err);
   }
   const uint32_t* gate = lean ? redo : nullptr;
   const int64_t X = (int64_t)R * L;

@@ -303,7 +303,8 @@ def decode_group_size(P: int, tiles_x_rows: int, limit: int) -> int:
 
 
 def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
-             out: torch.Tensor | None, acc: torch.Tensor | None = None) -> torch.Tensor:
+             out: torch.Tensor | None, acc: torch.Tensor | None = None,
+             stats: dict | None = None) -> torch.Tensor:
     """Verify + decrypt + decode + combine: out[r] = sum over p of the values of
     message r * P + p, mod the arena modulus (P = M / rows). With `acc` (int64
     [rows][L], contiguous) the sums are added to it instead (rounds done in waves).
@@ -313,6 +314,8 @@ def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
     1 KiB sub-chunk, element tiles are located in every message, and
     `k_decode_sum` accumulates each tile over all participants in LDS.
     Destroys the ciphertext (it is replaced by plaintext).
+    `stats` (a dict): receives "redo", the device word the lean kernels raise when a
+    stream is not canonical and the generic decoder recomputed the sums.
     """
     M, L, K, m = arena.M, arena.L, arena.K, arena.modulus
     if rows < 1 or M % rows:
@@ -337,6 +340,8 @@ def open_sum(arena: Arena, keys: KeySet, err: torch.Tensor, rows: int,
     redo = torch.zeros(1, dtype=torch.int32, device=dev)
     G.decode_sum(rows, P, Pg, L, m, arena.ct, arena.stride, arena.pt_len, pre, tile_sub, part,
                  out, err, redo, acc=acc)
+    if stats is not None:
+        stats["redo"] = redo
     return out if acc is None else acc
 
 

@@ -218,7 +218,7 @@ def test_one_pass_mac_block_edges(cuda, native):
             assert int(e2.item()) & 2, (L, pos)
 
 
-def _open_sum_case(native, cuda, rows_, P, L, m, gen):
+def _open_sum_case(native, cuda, rows_, P, L, m, gen, stats=None):
     """Host-sealed boxes (row-major: message r*P + p) -> open_sum vs a plain sum."""
     from sda_amd.ops.sealed import Arena, open_setup, open_sum
     keys = _keytable(native, cuda, 1)
@@ -232,7 +232,7 @@ def _open_sum_case(native, cuda, rows_, P, L, m, gen):
     kidx = torch.zeros(rows_ * P, dtype=torch.int32, device=cuda)
     ks = open_setup(arena, kidx, keys.sks, keys.pks, err)
     out = torch.empty(rows_, L, dtype=torch.int32, device=cuda)
-    open_sum(arena, ks, err, rows=rows_, out=out)
+    open_sum(arena, ks, err, rows=rows_, out=out, stats=stats)
     ref = torch.tensor(vals, dtype=torch.int64).view(rows_, P, L).sum(1) % m
     return int(err.item()), out.cpu().to(torch.int64), ref
 
@@ -284,20 +284,26 @@ def test_open_sum_canonical_streams(cuda, native, L, m, lean):
             return [(m - 1) if (i % 3) else 1 for i in range(L)]
         return torch.randint(0, m, (L,)).tolist()
     gpu().set_decode_lean(lean)
+    stats = {}
     try:
-        e, out, ref = _open_sum_case(native, cuda, 2, 11, L, m, gen)
+        e, out, ref = _open_sum_case(native, cuda, 2, 11, L, m, gen, stats)
     finally:
         gpu().set_decode_lean(1)
     assert e == 0
     assert torch.equal(out, ref)
+    # canonical streams stay on the lean kernels: nothing raised the fallback
+    assert int(stats["redo"].item()) == 0
 
 
 @pytest.mark.parametrize("swz", [0, 1])
-@pytest.mark.parametrize("L,m", [(6145, 433), (20000, 433), (30000, 8191), (20000, 746497),
-                                 (20000, 5038849)])
-def test_open_sum_accumulator_layouts(cuda, native, L, m, swz):
+@pytest.mark.parametrize("L,m,by_value", [(6145, 433, -1), (20000, 433, -1), (30000, 8191, -1),
+                                          (20000, 746497, 0), (20000, 746497, 1),
+                                          (20000, 5038849, 0), (20000, 5038849, 1),
+                                          (7, 746497, 1), (6145, 5038849, 1)])
+def test_open_sum_accumulator_layouts(cuda, native, L, m, swz, by_value):
     """The lean decode-sum kernels with plain and with padded (33-word) accumulator
-    rows, each forced for every modulus: both equal the plain sum."""
+    rows, each forced for every modulus, and for the long-code fields both the byte-wise
+    and the value-wise kernel: all equal the plain sum and none falls back."""
     from sda_amd._native import gpu
 
     def gen(j):
@@ -307,12 +313,16 @@ def test_open_sum_accumulator_layouts(cuda, native, L, m, swz):
             return [(m - 1) if (i % 5) else 0 for i in range(L)]
         return torch.randint(0, m, (L,)).tolist()
     gpu().set_decode_swz(swz)
+    gpu().set_decode_long(by_value)
+    stats = {}
     try:
-        e, out, ref = _open_sum_case(native, cuda, 2, 9, L, m, gen)
+        e, out, ref = _open_sum_case(native, cuda, 2, 9, L, m, gen, stats)
     finally:
         gpu().set_decode_swz(-1)
+        gpu().set_decode_long(-1)
     assert e == 0
     assert torch.equal(out, ref)
+    assert int(stats["redo"].item()) == 0
 
 
 def test_open_sum_foreign_encodings(cuda, native):
@@ -344,9 +354,17 @@ def test_open_sum_foreign_encodings(cuda, native):
             for i in range(j + 1, L, 1013):
                 row[i] = odd[i % len(odd)]
             return row
-        e, out, ref = _open_sum_case(native, cuda, 2, 5, L, m, gen_mid)
-        assert e == 0, (m, odd)
-        assert torch.equal(out, ref), (m, odd)
+        from sda_amd._native import gpu
+        for by_value in (0, 1):  # the byte-wise and the value-wise lean kernel both notice
+            gpu().set_decode_long(by_value)
+            stats = {}
+            try:
+                e, out, ref = _open_sum_case(native, cuda, 2, 5, L, m, gen_mid, stats)
+            finally:
+                gpu().set_decode_long(-1)
+            assert e == 0, (m, odd)
+            assert torch.equal(out, ref), (m, odd)
+            assert int(stats["redo"].item()) != 0, (m, odd, by_value)
 
 
 def test_open_sum_flags_wrong_length(cuda, native):
