@@ -528,7 +528,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
   constexpr int kWaveBytes = 64 * 64;
   constexpr int kPadShift = 5;  // one pad word per 32 ranks
   constexpr int kAccWords = kSwz ? kSumAcc + (kSumAcc >> kPadShift) + 1 : kSumAcc;
-  constexpr int kStageWords = kWaveBytes / 4 + 4;  // the pass from word 4 (16-byte aligned), the 4 bytes before it in word 3
+  // the pass from word 4 (16-byte aligned), the 4 bytes before it in word 3, four words after
+  // it (a window's second word; keeps the rows 16-byte aligned)
+  constexpr int kStageWords = kWaveBytes / 4 + 8;
   __shared__ uint32_t acc[kAccWords];
   constexpr int kBatch = 128;  // messages whose tile descriptors are staged at a time
   __shared__ uint32_t info[kBatch][4];
@@ -650,9 +652,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
       // next terminator is requested before the current one is worked on
       const uint8_t* mine = sbytes + 64 * lane - 3;
       auto window = [&](int p) {  // bytes p - 3 .. p of the lane: the terminator on top
-        uint32_t win;
-        __builtin_memcpy(&win, mine + p, 4);
-        return win;
+        // two aligned words and a byte shift (an unaligned LDS access costs several aligned ones)
+        const uint32_t off = (uint32_t)(mine + p - reinterpret_cast<const uint8_t*>(&stage[wave][0]));
+        const uint32_t* q = &stage[wave][off >> 2];
+        return __builtin_amdgcn_alignbyte(q[1], q[0], off & 3u);
       };
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
