@@ -528,13 +528,16 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
   constexpr int kWaveBytes = 64 * 64;
   constexpr int kPadShift = 5;  // one pad word per 32 ranks
   constexpr int kAccWords = kSwz ? kSumAcc + (kSumAcc >> kPadShift) + 1 : kSumAcc;
-  // the pass from word 4 (16-byte aligned), the 4 bytes before it in word 3, four words after
-  // it (a window's second word; keeps the rows 16-byte aligned)
-  constexpr int kStageWords = kWaveBytes / 4 + 8;
+  // a lane's slot: the 4 bytes before its 64 (its neighbour's last word, or the bytes before
+  // the pass) and the 64, 17 words -- an odd stride, so that the lanes' window reads, each
+  // inside its own slot, fall into different banks (side by side, 16 words apart, every
+  // read was a 32-way conflict); one more word after the last slot for a window's second
+  constexpr int kSlotWords = 17;
+  constexpr int kStageWords = 64 * kSlotWords + 1;
   __shared__ uint32_t acc[kAccWords];
   constexpr int kBatch = 128;  // messages whose tile descriptors are staged at a time
   __shared__ uint32_t info[kBatch][4];
-  __shared__ __attribute__((aligned(16))) uint32_t stage[kWaves][kStageWords];
+  __shared__ uint32_t stage[kWaves][kStageWords];
   auto add = [&](uint32_t byte_off, uint32_t v) {
     lds_add(acc, kSwz ? byte_off + ((byte_off >> (kPadShift + 2)) << 2) : byte_off, v);
   };
@@ -544,8 +547,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
   const uint32_t E0 = (uint32_t)t * kSumTile;
   const uint32_t W = min((uint32_t)kSumTile, (uint32_t)L - E0);
   for (int i = tid; i < kAccWords; i += kBlock) acc[i] = 0;
-  // this wave's staging area
-  uint8_t* const sbytes = reinterpret_cast<uint8_t*>(&stage[wave][4]);
+  uint32_t* const slot = &stage[wave][kSlotWords * lane];  // this lane's: [0] history, [1..16] bytes
   const int pbeg = g * Pg, pend = min(P, pbeg + Pg);
   uint32_t bad = 0;
   bool malformed = false;
@@ -620,10 +622,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        *reinterpret_cast<uint4*>(sbytes + 64 * lane + 16 * q) =
-            make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-      if (lane == 0) stage[wave][3] = wave_prev;
+      for (int q = 0; q < 16; ++q) slot[1 + q] = w[q];
+      if (lane < 63) slot[kSlotWords] = w[15];  // the next lane's history
+      if (lane == 0) slot[0] = wave_prev;
       const uint64_t traw = term_mask64(w);
       const uint64_t tmask = traw & byte_range_mask(lo, hi);
       // too long a code: kMaxBytes continuation bytes in a row, within the lane ...
@@ -650,11 +651,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       // the lane's terminators, low half of its bytes then high half; the window of the
       // next terminator is requested before the current one is worked on
-      const uint8_t* mine = sbytes + 64 * lane - 3;
       auto window = [&](int p) {  // bytes p - 3 .. p of the lane: the terminator on top
         // two aligned words and a byte shift (an unaligned LDS access costs several aligned ones)
-        const uint32_t off = (uint32_t)(mine + p - reinterpret_cast<const uint8_t*>(&stage[wave][0]));
-        const uint32_t* q = &stage[wave][off >> 2];
+        const uint32_t off = (uint32_t)p + 1u;  // byte offset in the slot of byte p - 3
+        const uint32_t* q = slot + (off >> 2);
         return __builtin_amdgcn_alignbyte(q[1], q[0], off & 3u);
       };
 #pragma unroll
