@@ -651,34 +651,52 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       // the lane's terminators, low half of its bytes then high half; the window of the
       // next terminator is requested before the current one is worked on
-      auto window = [&](int p) {  // bytes p - 3 .. p of the lane: the terminator on top
-        // two aligned words and a byte shift (an unaligned LDS access costs several aligned ones)
+      // A value's window -- bytes p - 3 .. p of the lane, the terminator on top -- is two
+      // aligned words and a byte shift (an unaligned LDS access costs several aligned ones),
+      // requested one turn ahead and put together only when used.
+      struct Window {
+        uint32_t lo, hi, sh;
+      };
+      auto request = [&](int p) {
         const uint32_t off = (uint32_t)p + 1u;  // byte offset in the slot of byte p - 3
         const uint32_t* q = slot + (off >> 2);
-        return __builtin_amdgcn_alignbyte(q[1], q[0], off & 3u);
+        return Window{q[0], q[1], off & 3u};
       };
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        uint32_t tm = half ? (uint32_t)(tmask >> 32) : (uint32_t)tmask;
-        uint32_t next = tm != 0 ? window(__builtin_ctz(tm) + 32 * half) : 0u;
-        while (__builtin_amdgcn_ballot_w64(tm != 0) != 0) {
-          if (tm != 0) {
-            const uint32_t win = next;
-            tm &= tm - 1;
-            if (tm != 0) next = window(__builtin_ctz(tm) + 32 * half);
-            const uint32_t m7 = win >> 7;
-            const uint32_t c2 = (m7 >> 16) & 1u;   // byte p - 1 continues
-            const uint32_t c1 = (m7 >> 8) & c2;    // ... and p - 2
-            const uint32_t c0 = m7 & c1;           // ... and p - 3
-            const uint32_t rl = c2 + c1 + c0;
-            const uint32_t g7 = win & 0x7f7f7f7fu;
-            const uint32_t x = (g7 & 0x007f007fu) | ((g7 & 0x7f007f00u) >> 1);
-            const uint32_t full = (x & 0x3fffu) | ((x >> 2) & 0x0fffc000u);
-            const uint32_t z = full >> (21u - 7u * rl);
-            bad |= z & 1u;  // odd: a negative value
-            add(a4, z);
-            a4 += 4u;
-          }
+      auto emit = [&](const Window& wd, uint32_t at) {
+        const uint32_t win = __builtin_amdgcn_alignbyte(wd.hi, wd.lo, wd.sh);
+        const uint32_t m7 = win >> 7;
+        const uint32_t c2 = (m7 >> 16) & 1u;   // byte p - 1 continues
+        const uint32_t c1 = (m7 >> 8) & c2;    // ... and p - 2
+        const uint32_t c0 = m7 & c1;           // ... and p - 3
+        const uint32_t rl = c2 + c1 + c0;
+        const uint32_t g7 = win & 0x7f7f7f7fu;
+        const uint32_t x = (g7 & 0x007f007fu) | ((g7 & 0x7f007f00u) >> 1);
+        const uint32_t full = (x & 0x3fffu) | ((x >> 2) & 0x0fffc000u);
+        const uint32_t z = full >> (21u - 7u * rl);
+        bad |= z & 1u;  // odd: a negative value
+        add(at, z);
+      };
+      // both halves of the lane's bytes side by side: one terminator of each per turn (two
+      // independent chains, half the loop turns)
+      uint32_t t0 = (uint32_t)tmask, t1 = (uint32_t)(tmask >> 32);
+      uint32_t a40 = a4, a41 = a4 + 4u * (uint32_t)__popc(t0);
+      Window n0 = {0, 0, 0}, n1 = {0, 0, 0};
+      if (t0 != 0) n0 = request(__builtin_ctz(t0));
+      if (t1 != 0) n1 = request(__builtin_ctz(t1) + 32);
+      while (__builtin_amdgcn_ballot_w64((t0 | t1) != 0) != 0) {
+        const Window w0 = n0, w1 = n1;
+        const bool h0 = t0 != 0, h1 = t1 != 0;
+        t0 &= t0 - 1;
+        t1 &= t1 - 1;
+        if (t0 != 0) n0 = request(__builtin_ctz(t0));
+        if (t1 != 0) n1 = request(__builtin_ctz(t1) + 32);
+        if (h0) {
+          emit(w0, a40);
+          a40 += 4u;
+        }
+        if (h1) {
+          emit(w1, a41);
+          a41 += 4u;
         }
       }
       rank += total;

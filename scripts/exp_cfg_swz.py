@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Experiment: a benchmark configuration's rounds with the lean decode-sum's accumulator
-rows plain and padded (usage: exp_cfg_swz.py CONFIG): wall time per round."""
+rows plain and padded, or (with `long`) its byte-wise and value-wise long-code kernels
+(usage: exp_cfg_swz.py CONFIG [long]): wall time per round."""
 import os
 import sys
 import time
@@ -18,8 +19,10 @@ eng = DeviceAggregator(spec)
 g = torch.Generator(device="cuda").manual_seed(1)
 x = torch.randint(0, spec.field_modulus, (cfg.participants, spec.dimension), dtype=torch.int32,
                   device="cuda", generator=g)
+which = "long" if len(sys.argv) > 2 and sys.argv[2] == "long" else "swz"
+setter = gpu().set_decode_long if which == "long" else gpu().set_decode_swz
 for mode in (0, 1, 0, 1):
-    gpu().set_decode_swz(mode)
+    setter(mode)
     for _ in range(2):
         eng.run_round(x, check=True)
     torch.cuda.synchronize()
@@ -27,6 +30,6 @@ for mode in (0, 1, 0, 1):
     for _ in range(5):
         eng.run_round(x, check=False)
     torch.cuda.synchronize()
-    print(f"config {cfg.number if hasattr(cfg, 'number') else sys.argv[1]} decode swz {mode}: "
+    print(f"config {sys.argv[1]} decode {which} {mode}: "
           f"{(time.perf_counter() - t0) / 5 * 1e3:.2f} ms/round", flush=True)
-gpu().set_decode_swz(-1)
+setter(-1)
