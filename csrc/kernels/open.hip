@@ -144,6 +144,23 @@ __global__ void __launch_bounds__(kBlock)
     for (uint64_t t = ((uint64_t)tot + kSumTile - 1) / kSumTile; t <= (uint64_t)T; ++t) row[t] = (uint32_t)S;
 }
 
+// Workgroup -> (element tile, row, participant group) of the decode + sum kernels' grid
+// (tiles, rows, groups). Workgroups are handed out in grid order, x fastest, round-robin over
+// the 8 XCDs: with two tiles a row -- boxes of 10,000 values are a tile of 6,144 and one of
+// 3,856 -- every first tile went to the even XCDs and every second one to the odd ones, which
+// then waited for the even ones to finish. With fewer than 8 tiles a row the tile index
+// therefore runs slowest: all the rows' first tiles, then all their second ones.
+struct SumTileId {
+  int t, r, g;
+};
+SDA_DEV SumTileId sum_tile_id() {
+  const unsigned T = gridDim.x, R = gridDim.y, G = gridDim.z;
+  if (T >= 8u || (uint64_t)T * R * G >= (1ull << 31)) return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+  const unsigned n = blockIdx.x + T * (blockIdx.y + R * blockIdx.z), RG = R * G;
+  const unsigned t = n / RG, rest = n - t * RG, g = rest / R;
+  return {(int)t, (int)(rest - g * R), (int)g};
+}
+
 // Each wave walks its own participants (round-robin over the group) in 4 KiB
 // passes -- 64 lanes x 64 bytes, ranks by a wave scan -- so no block barrier
 // sits between a pass's loads and the next: 16 independent waves per CU keep
@@ -155,7 +172,8 @@ SDA_DEV void decode_sum_body(AccT* acc, uint32_t (*info)[4], int L, int P, int P
                              const uint32_t* __restrict__ pre, const uint32_t* __restrict__ tile_sub,
                              AccT* __restrict__ part, uint32_t* err) {
   constexpr int kWaveBytes = 64 * 64;
-  const int t = blockIdx.x, r = blockIdx.y, g = blockIdx.z, R = gridDim.y;
+  const SumTileId id = sum_tile_id();
+  const int t = id.t, r = id.r, g = id.g, R = gridDim.y;
   const int T = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t E0 = (uint32_t)t * kSumTile;
@@ -294,7 +312,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   auto add = [&](uint32_t byte_off, uint32_t v) {
     lds_add(acc, kSwz ? byte_off + ((byte_off >> (kPadShift + 2)) << 2) : byte_off, v);
   };
-  const int t = blockIdx.x, r = blockIdx.y, g = blockIdx.z, R = gridDim.y;
+  const SumTileId id = sum_tile_id();
+  const int t = id.t, r = id.r, g = id.g, R = gridDim.y;
   const int T = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t E0 = (uint32_t)t * kSumTile;
@@ -541,7 +560,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
   auto add = [&](uint32_t byte_off, uint32_t v) {
     lds_add(acc, kSwz ? byte_off + ((byte_off >> (kPadShift + 2)) << 2) : byte_off, v);
   };
-  const int t = blockIdx.x, r = blockIdx.y, g = blockIdx.z, R = gridDim.y;
+  const SumTileId id = sum_tile_id();
+  const int t = id.t, r = id.r, g = id.g, R = gridDim.y;
   const int T = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t E0 = (uint32_t)t * kSumTile;

@@ -98,15 +98,31 @@ SDA_DEV void load_values(uint32_t (&v)[kValuesPerLane], const VT* src, int e0, i
 // i.e. six / four / three workgroups a CU; the issue-bound kernel ran at 57 % of its
 // VALU peak with three -- and a value past the bound (a caller's error: the slots of
 // the arena are sized by the same bound) is encoded as zero rather than overrun it.
+// Whether the messages' ends (the values behind their last whole tile) go four to a workgroup,
+// and the grid that follows from it: whole tiles first, then the ends.
+template <bool MAC>
+__host__ __device__ inline bool encode_short_ends(int L) {
+  const int r = L % kEncodeValues;
+  return !MAC && r > 0 && r <= kEncodeValues / kWaves;
+}
+template <bool MAC>
+static unsigned encode_grid(int M, int L) {
+  const unsigned whole = (unsigned)(L / kEncodeValues) * (unsigned)M;
+  if (L % kEncodeValues == 0) return whole;
+  return whole + (encode_short_ends<MAC>(L) ? (unsigned)(M + kWaves - 1) / kWaves : (unsigned)M);
+}
+
 template <typename VT, bool MAC, int kMaxB>
 __global__ void __launch_bounds__(kBlock)
-    k_encode_encrypt(int L, const VT* __restrict__ vals, const uint32_t* __restrict__ tile_off,
+    k_encode_encrypt(int L, int M, const VT* __restrict__ vals, const uint32_t* __restrict__ tile_off,
                      const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct, uint64_t stride,
                      const uint32_t* __restrict__ pows, const uint32_t* __restrict__ pt_len,
                      uint32_t* __restrict__ partials, int K) {
   static_assert(kMaxB >= 3 && kMaxB <= 5 && (sizeof(VT) > 2 || kMaxB == 3), "code length bound");
   constexpr uint32_t kBound = kMaxB == 5 ? 0xffffffffu : (1u << (7 * kMaxB - 1)) - 1u;  // largest value
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kEncodeValues * kMaxB + 128];
+  // a wave's part of the tile where the waves work on their own (below)
+  constexpr int kWaveBytes = kEncodeValues / kWaves * kMaxB + 128;  // as a tile: room for the offset in the first block
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kWaves * kWaveBytes];
   __shared__ uint32_t scratch[kWaves];
   // chunks a tile can touch: its bytes span at most 2 + (tile bytes - 2) / chunk bytes
   constexpr int kSlots = sizeof(VT) <= 2 ? 3 : 4;
@@ -115,16 +131,65 @@ __global__ void __launch_bounds__(kBlock)
     int32_t* flat = &cacc[0][0][0];
     for (int i = threadIdx.x; i < kSlots * 16 * (kPolyDigits + 1); i += kBlock) flat[i] = 0;
   }
-  const int t = blockIdx.x, j = blockIdx.y;
   const int T = (L + kTileValues - 1) / kTileValues;  // count tiles per message
-  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  // Workgroup -> (tile, message): first every message's whole tiles, the message index running
+  // fastest where messages are short, then the ends (encode_grid). Workgroups go round-robin over the 8 XCDs; with
+  // the tile index fastest, messages of two tiles -- a whole one and a short end, the boxes of
+  // the many-clerk rounds -- sent every whole tile to the even XCDs and every end to the odd
+  // ones, which then stood idle: the kernel took as long as half the chip needs for the whole
+  // tiles (3.0 ps a value for boxes of 10,000 values, 2.2 for boxes of ten whole tiles).
+  // Short ends: where a message's end has no more than a wave's 2048 values, a workgroup takes
+  // the ends of four messages, a wave each, instead of keeping an LDS tile and four wave slots
+  // busy with one or two waves at work. `un` threads numbered `tid` work on one tile: the
+  // workgroup's 256, or a wave's 64.
+  const int whole = L / kEncodeValues, b = blockIdx.x;
+  const bool ends = b >= whole * M && encode_short_ends<MAC>(L);  // block-uniform
+  int t, jw;
+  if (b < whole * M) {
+    if (whole < 8) {  // few tiles a message: the message index runs fastest
+      t = b / M;
+      jw = b - t * M;
+    } else {  // long messages: tile by tile (4 % faster there: neighbours in time are neighbours in memory)
+      jw = b / whole;
+      t = b - jw * whole;
+    }
+  } else {
+    t = whole;
+    jw = ends ? kWaves * (b - whole * M) + wave : b - whole * M;
+  }
+  const bool idle = jw >= M;  // a wave without a message: no values, stores nothing
+  const int j = idle ? M - 1 : jw;
+  const int tid = ends ? lane : (int)threadIdx.x;
+  const int un = ends ? 64 : kBlock;
+  uint8_t* lds = ends ? tile + wave * kWaveBytes : tile;
+  const int Lv = idle ? t * kEncodeValues : L;  // the values this unit sees
   const int e0 = t * kEncodeValues + tid * kValuesPerLane;
   const VT* src = vals + (size_t)j * L;
+  // the tile's offset and the message's key: uniform loads, asked for here so that they arrive
+  // with the values instead of each costing the workgroup a memory latency of its own later
+  const uint32_t a = tile_off[(size_t)j * T + t * (kEncodeValues / kTileValues)];
+  const MsgKey key = keys[j];
   // full: all 32 values present (the lane's values are then in registers); a tile's
   // last lane with values takes the rolled loops below, straight from memory, and
   // the lanes past the message's end (most of a short message's last tile) nothing
-  const bool full = e0 + kValuesPerLane <= L;
-  const int nv = full ? kValuesPerLane : max(0, L - e0);
+  const bool full = e0 + kValuesPerLane <= Lv;
+  // The message's last values, fewer than a lane's 32: spread one by one over the lanes from the
+  // first one without its 32 on, which have nothing else to do (more than one each only where
+  // that lane sits at the very end of a tile). Lanes are scanned in order, so the bytes land
+  // where they belong. One lane walking up to 31 values through two rolled loops of dependent
+  // loads kept its whole workgroup, LDS tile and all, on the CU for ~20 us: as long as a full
+  // tile takes, for every box whose length is no multiple of 32.
+  int eg = e0, nv = kValuesPerLane;
+  if (!full) {
+    const int left = Lv - t * kEncodeValues;     // this tile's values (< kEncodeValues here)
+    const int tl = left / kValuesPerLane;        // first lane without its 32: tid >= tl
+    const int nt = left - tl * kValuesPerLane;   // 0..31 values for lanes tl..un-1
+    const int c = (nt + (un - tl) - 1) / (un - tl);
+    const int r = tid - tl;
+    eg = t * kEncodeValues + tl * kValuesPerLane + r * c;
+    nv = max(0, min(c, nt - r * c));
+  }
   uint32_t v[kValuesPerLane];            // the lane's values (u8 / u32 storage)
   uint32_t pr[kValuesPerLane / 2] = {};  // u16 storage: the lane's values as pairs, as loaded
   // Fast lanes (all 32 values present and < 2^13, i.e. 1- or 2-byte varints of
@@ -203,14 +268,28 @@ __global__ void __launch_bounds__(kBlock)
   } else if (!fast) {
 #pragma unroll 1
     for (int i = 0; i < nv; ++i) {
-      const uint32_t x = (uint32_t)src[e0 + i];
+      const uint32_t x = (uint32_t)src[eg + i];
       const uint64_t z = (uint64_t)(x > kBound ? 0u : x) << 1;
       my_bytes += 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
     }
   }
-  uint32_t tile_bytes;
-  const uint32_t excl = block_excl_scan(my_bytes, scratch, &tile_bytes);
-  const uint32_t a = tile_off[(size_t)j * T + t * (kEncodeValues / kTileValues)];
+  // byte offsets within the tile: a scan over the wave, and over the waves before it where
+  // the workgroup shares the tile
+  uint32_t tile_bytes, excl;
+  {
+    const uint32_t inc = wave_incl_scan(my_bytes);
+    if (lane == 63) scratch[wave] = inc;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kWaves; ++i) {
+      const uint32_t sum = scratch[i];
+      if (i < wave) before += sum;
+      tot += sum;
+    }
+    excl = (ends ? 0u : before) + inc - my_bytes;
+    tile_bytes = ends ? scratch[wave] : tot;
+  }
   const uint32_t b0 = (32u + a) >> 6;
   const uint32_t base = 32u + a - 64u * b0;  // LDS index of message byte `a`
   uint32_t pos = base + excl;
@@ -284,7 +363,7 @@ __global__ void __launch_bounds__(kBlock)
   } else {
 #pragma unroll 1
     for (int i = 0; i < nv; ++i) {
-      const uint32_t x = (uint32_t)src[e0 + i];
+      const uint32_t x = (uint32_t)src[eg + i];
       const uint64_t z = (uint64_t)(x > kBound ? 0u : x) << 1;
       const uint32_t len = 1u + (z >= (1ull << 7)) + (z >= (1ull << 14)) + (z >= (1ull << 21)) + (z >= (1ull << 28));
 #pragma unroll
@@ -297,7 +376,6 @@ __global__ void __launch_bounds__(kBlock)
   __syncthreads();
   // MAC operands that depend only on the tile's position: requested here, so that
   // their latency is spent under the keystream computation
-  const int wave = tid >> 6, lane = tid & 63;
   const int row = lane & 15, g = lane >> 4;
   const uint32_t ks0 = 32u + a, ks1 = ks0 + tile_bytes;  // the tile's keystream byte range
   const int kf = (int)(ks0 / kChunkBytes), kl = (int)((ks1 - 1u) / kChunkBytes);
@@ -330,11 +408,10 @@ __global__ void __launch_bounds__(kBlock)
       }
     }
   }
-  const MsgKey key = keys[j];
   // what the message's blocks have in common of their first double round (scalar unit)
   const SalsaPrefix pre = salsa20_prefix(key.subkey, key.nonce[0], key.nonce[1]);
   const uint32_t nblk = (base + tile_bytes + 63) >> 6;
-  for (uint32_t blk = tid; blk < nblk; blk += kBlock) {
+  for (uint32_t blk = tid; blk < nblk; blk += un) {
     uint32_t w[16];
     salsa20_block(w, pre, key.subkey, key.nonce[0], key.nonce[1], b0 + blk);
     uint4* q = reinterpret_cast<uint4*>(lds + 64 * blk);
@@ -360,7 +437,7 @@ __global__ void __launch_bounds__(kBlock)
   if constexpr (MAC) __builtin_amdgcn_s_setprio(3);
   uint8_t* gmsg = ct + (size_t)j * stride + 48;
   const uint32_t lo = a & ~15u, hi = (a + tile_bytes + 15u) & ~15u, end = a + tile_bytes;
-  for (uint32_t c = lo + 16u * tid; c < hi; c += 16u * kBlock) {
+  for (uint32_t c = lo + 16u * tid; c < hi; c += 16u * un) {
     if (c >= a && c + 16u <= end) {
       *reinterpret_cast<uint4*>(gmsg + c) = *reinterpret_cast<const uint4*>(lds + (c - a + base));
     } else {
@@ -1101,14 +1178,15 @@ void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, uint32_t exp
 }
 
 template <typename VT, int kMaxB>
-static void launch_encode_t(dim3 grid, int L, const void* vals, const uint32_t* tile_off,
+static void launch_encode_t(int M, int L, const void* vals, const uint32_t* tile_off,
                             const MsgKey* keys, uint8_t* ct, uint64_t stride, const uint32_t* pows,
                             const uint32_t* pt_len, uint32_t* partials, int K, hipStream_t s) {
   if (pows && pt_len && partials)
-    hipLaunchKernelGGL((k_encode_encrypt<VT, true, (sizeof(VT) > 2 ? 5 : 3)>), grid, dim3(kBlock), 0, s, L,
-                       (const VT*)vals, tile_off, keys, ct, stride, pows, pt_len, partials, K);
+    hipLaunchKernelGGL((k_encode_encrypt<VT, true, (sizeof(VT) > 2 ? 5 : 3)>), dim3(encode_grid<true>(M, L)),
+                       dim3(kBlock), 0, s, L, M, (const VT*)vals, tile_off, keys, ct, stride, pows, pt_len, partials, K);
   else
-    hipLaunchKernelGGL((k_encode_encrypt<VT, false, kMaxB>), grid, dim3(kBlock), 0, s, L, (const VT*)vals,
+    hipLaunchKernelGGL((k_encode_encrypt<VT, false, kMaxB>), dim3(encode_grid<false>(M, L)), dim3(kBlock), 0, s, L,
+                       M, (const VT*)vals,
                        tile_off, keys, ct, stride, pows, pt_len, partials, K);
 }
 
@@ -1117,17 +1195,16 @@ void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
                            uint64_t stride, const uint32_t* pows, const uint32_t* pt_len,
                            uint32_t* partials, int K, int max_code_bytes, hipStream_t s) {
   if (M <= 0 || L <= 0) return;
-  dim3 grid((L + kEncodeValues - 1) / kEncodeValues, M);
   if (value_bytes == 1)
-    launch_encode_t<uint8_t, 3>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
+    launch_encode_t<uint8_t, 3>(M, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
   else if (value_bytes == 2)
-    launch_encode_t<uint16_t, 3>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
+    launch_encode_t<uint16_t, 3>(M, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
   else if (max_code_bytes <= 3)
-    launch_encode_t<uint32_t, 3>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
+    launch_encode_t<uint32_t, 3>(M, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
   else if (max_code_bytes == 4)
-    launch_encode_t<uint32_t, 4>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
+    launch_encode_t<uint32_t, 4>(M, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
   else
-    launch_encode_t<uint32_t, 5>(grid, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
+    launch_encode_t<uint32_t, 5>(M, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
 }
 
 extern int g_powers_prio;  // keys.hip (set_key_prio)

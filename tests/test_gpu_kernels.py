@@ -102,7 +102,10 @@ def test_seal_setup_forms_open_on_host(cuda, native, many, tables):
 @pytest.mark.parametrize("L,modulus", [(1, 433), (10, 433), (5000, 433), (20000, 433),
                                        (3000, 2 ** 31 - 1), (70000, 65521), (150001, 433),
                                        (40000, 2 ** 31 - 1), (25000, 5038849), (7, 746497),
-                                       (8192, (1 << 27) - 39)])
+                                       (8192, (1 << 27) - 39),
+                                       # a message's last values (fewer than a lane's 32) are spread over
+                                       # the lanes behind them: few such lanes left at a tile's end
+                                       (8191, 433), (8145, 746497), (16382, 5038849)])
 def test_gpu_seal_opens_on_host(cuda, native, monkeypatch, L, modulus, fused):
     """GPU-sealed boxes open on the host. `fused`: the tag's middle chunks computed
     inside the encode kernel (per tile, in LDS) instead of by a pass over the
