@@ -1176,9 +1176,33 @@ __global__ void __launch_bounds__(kBlock)
 
 }  // namespace
 
+// Rows of a few entries (the many-clerk boxes: three byte counts, a handful of terminator
+// counts): a thread per row. A 256-thread workgroup per row, scan and two barriers for three
+// numbers, was 0.17 ms a call over 728,000 rows.
+__global__ void __launch_bounds__(kBlock) k_segscan_rows(int M, int T, uint32_t* __restrict__ data,
+                                                         uint32_t* __restrict__ totals, uint32_t expect,
+                                                         uint32_t* err) {
+  const int j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= M) return;
+  uint32_t* row = data + (size_t)j * T;
+  uint32_t carry = 0;
+  for (int i = 0; i < T; ++i) {
+    const uint32_t v = row[i];
+    row[i] = carry;
+    carry += v;
+  }
+  if (totals) totals[j] = carry;
+  if (err && carry != expect) atomicOr(err, kErrMalformed);
+}
+
 void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, uint32_t expect, uint32_t* err,
                     hipStream_t s) {
   if (M <= 0) return;
+  if (T <= 64 && M >= 4096) {
+    hipLaunchKernelGGL(k_segscan_rows, dim3((M + kBlock - 1) / kBlock), dim3(kBlock), 0, s, M, T, data, totals,
+                       expect, err);
+    return;
+  }
   hipLaunchKernelGGL(k_segscan, dim3(M), dim3(kBlock), 0, s, T, data, totals, expect, err);
 }
 

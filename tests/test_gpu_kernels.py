@@ -607,3 +607,25 @@ def test_round_pss_dropout(cuda):
 def test_round_pss_fullmask(cuda):
     from sda_amd.models import AggregationSpec, PSS_4_8_3, FullMask
     _round(cuda, AggregationSpec(2000, 433, PSS_4_8_3, FullMask(433)), 3)
+
+
+@pytest.mark.parametrize("M,T", [(7, 3), (5000, 3), (5000, 16), (4096, 1), (300, 700), (5000, 64), (5000, 65)])
+def test_segscan_rows(cuda, native, M, T):
+    """Row-wise exclusive scan: the workgroup-per-row kernel and the thread-per-row one
+    (many short rows) against torch.cumsum; a row off its expected sum raises the error word."""
+    from sda_amd.ops import gpu as G
+    data = torch.randint(0, 1000, (M, T), dtype=torch.int32)
+    data[:, -1] += 100_000 - data.sum(dim=1, dtype=torch.int32)  # every row sums to 100,000
+    want = torch.cumsum(data, dim=1, dtype=torch.int64) - data
+    d = data.to(cuda)
+    totals = torch.empty(M, dtype=torch.int32, device=cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    G.segscan(d, totals, expect=100_000, err=err)
+    assert torch.equal(d.cpu().to(torch.int64), want)
+    assert torch.equal(totals.cpu(), torch.full((M,), 100_000, dtype=torch.int32))
+    assert int(err.item()) == 0
+    bad = data.clone()
+    bad[M // 2, 0] += 1
+    d = bad.to(cuda)
+    G.segscan(d, totals, expect=100_000, err=err)
+    assert int(err.item()) != 0
