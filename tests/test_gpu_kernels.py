@@ -105,7 +105,9 @@ def test_seal_setup_forms_open_on_host(cuda, native, many, tables):
                                        (8192, (1 << 27) - 39),
                                        # a message's last values (fewer than a lane's 32) are spread over
                                        # the lanes behind them: few such lanes left at a tile's end
-                                       (8191, 433), (8145, 746497), (16382, 5038849)])
+                                       (8191, 433), (8145, 746497), (16382, 5038849),
+                                       # ends of at most a wave's 2048 values go four to a workgroup
+                                       (2048, 433), (2047, 746497), (2049, 433), (10240, 5038849)])
 def test_gpu_seal_opens_on_host(cuda, native, monkeypatch, L, modulus, fused):
     """GPU-sealed boxes open on the host. `fused`: the tag's middle chunks computed
     inside the encode kernel (per tile, in LDS) instead of by a pass over the
