@@ -120,9 +120,17 @@ __global__ void __launch_bounds__(kBlock)
                      uint32_t* __restrict__ partials, int K) {
   static_assert(kMaxB >= 3 && kMaxB <= 5 && (sizeof(VT) > 2 || kMaxB == 3), "code length bound");
   constexpr uint32_t kBound = kMaxB == 5 ? 0xffffffffu : (1u << (7 * kMaxB - 1)) - 1u;  // largest value
+  // Five-byte codes: the tile goes through LDS in two passes, the first two waves' values and
+  // then the other two's (all four waves on the keystream and the stores of either pass), so
+  // that LDS holds half a tile, 21 KB instead of 41, and five workgroups fit a CU instead of
+  // three: 4.45 -> 4.03 ms for 1000 boxes of a million values below 2^31. Not for four-byte
+  // codes (33 KB, four workgroups a CU in one pass): the extra barriers and the passes with two
+  // waves scattering cost what the fifth workgroup gives (1.07 against 1.10 ms).
+  constexpr int kPasses = (!MAC && kMaxB >= 5) ? 2 : 1;
+  constexpr int kPassWaves = kWaves / kPasses;
   // a wave's part of the tile where the waves work on their own (below)
   constexpr int kWaveBytes = kEncodeValues / kWaves * kMaxB + 128;  // as a tile: room for the offset in the first block
-  __shared__ __attribute__((aligned(16))) uint8_t tile[kWaves * kWaveBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kPassWaves * kWaveBytes];
   __shared__ uint32_t scratch[kWaves];
   // chunks a tile can touch: its bytes span at most 2 + (tile bytes - 2) / chunk bytes
   constexpr int kSlots = sizeof(VT) <= 2 ? 3 : 4;
@@ -162,13 +170,13 @@ __global__ void __launch_bounds__(kBlock)
   const int j = idle ? M - 1 : jw;
   const int tid = ends ? lane : (int)threadIdx.x;
   const int un = ends ? 64 : kBlock;
-  uint8_t* lds = ends ? tile + wave * kWaveBytes : tile;
+  uint8_t* lds = ends ? tile + (wave % kPassWaves) * kWaveBytes : tile;
   const int Lv = idle ? t * kEncodeValues : L;  // the values this unit sees
   const int e0 = t * kEncodeValues + tid * kValuesPerLane;
   const VT* src = vals + (size_t)j * L;
   // the tile's offset and the message's key: uniform loads, asked for here so that they arrive
   // with the values instead of each costing the workgroup a memory latency of its own later
-  const uint32_t a = tile_off[(size_t)j * T + t * (kEncodeValues / kTileValues)];
+  const uint32_t a_tile = tile_off[(size_t)j * T + t * (kEncodeValues / kTileValues)];
   const MsgKey key = keys[j];
   // full: all 32 values present (the lane's values are then in registers); a tile's
   // last lane with values takes the rolled loops below, straight from memory, and
@@ -275,24 +283,39 @@ __global__ void __launch_bounds__(kBlock)
   }
   // byte offsets within the tile: a scan over the wave, and over the waves before it where
   // the workgroup shares the tile
-  uint32_t tile_bytes, excl;
-  {
-    const uint32_t inc = wave_incl_scan(my_bytes);
-    if (lane == 63) scratch[wave] = inc;
-    __syncthreads();
-    uint32_t before = 0, tot = 0;
+  const uint32_t inc = wave_incl_scan(my_bytes);
+  if (lane == 63) scratch[wave] = inc;
+  __syncthreads();
+  uint32_t wsum[kWaves], before = 0;  // the waves' bytes; those of the waves before this one
 #pragma unroll
-    for (int i = 0; i < kWaves; ++i) {
-      const uint32_t sum = scratch[i];
-      if (i < wave) before += sum;
-      tot += sum;
-    }
-    excl = (ends ? 0u : before) + inc - my_bytes;
-    tile_bytes = ends ? scratch[wave] : tot;
+  for (int i = 0; i < kWaves; ++i) {
+    wsum[i] = scratch[i];
+    if (i < wave) before += wsum[i];
   }
+#pragma unroll 1
+  for (int pass = 0; pass < kPasses; ++pass) {
+  // `mine`: this wave's values are in this pass (wave-uniform); `work`: it takes part in the
+  // pass's keystream and stores (a wave on its own message end: only in its own pass)
+  const bool mine = kPasses == 1 || wave / kPassWaves == pass;
+  const bool work = !ends || mine;
+  uint32_t pass_before = 0, pass_bytes = 0;  // of the shared tile: bytes before this pass, and in it
+#pragma unroll
+  for (int i = 0; i < kWaves; ++i) {
+    if (i < pass * kPassWaves) pass_before += wsum[i];
+    else if (i < (pass + 1) * kPassWaves) pass_bytes += wsum[i];
+  }
+  const uint32_t a = ends ? a_tile : a_tile + pass_before;  // message byte where this pass's bytes begin
+  const uint32_t tile_bytes = ends ? wsum[wave] : pass_bytes;
   const uint32_t b0 = (32u + a) >> 6;
   const uint32_t base = 32u + a - 64u * b0;  // LDS index of message byte `a`
-  uint32_t pos = base + excl;
+  uint32_t pos = base + (ends ? 0u : before - pass_before) + inc - my_bytes;
+  if (mine) {
+  if constexpr (kPasses > 1) {
+    // keeps the compiler from computing every code byte of both passes ahead of the loop
+    // (256 registers and one wave a SIMD): the values "change" here
+#pragma unroll
+    for (int i = 0; i < kValuesPerLane; ++i) asm volatile("" : "+v"(v[i]));
+  }
   if (fast) {
     if constexpr (sizeof(VT) == 2) {
       // Per pair: both 16-bit codes (byte 0 = low 7 bits of z = 2 v plus the
@@ -373,6 +396,7 @@ __global__ void __launch_bounds__(kBlock)
       pos += len;
     }
   }
+  }  // mine
   __syncthreads();
   // MAC operands that depend only on the tile's position: requested here, so that
   // their latency is spent under the keystream computation
@@ -410,7 +434,7 @@ __global__ void __launch_bounds__(kBlock)
   }
   // what the message's blocks have in common of their first double round (scalar unit)
   const SalsaPrefix pre = salsa20_prefix(key.subkey, key.nonce[0], key.nonce[1]);
-  const uint32_t nblk = (base + tile_bytes + 63) >> 6;
+  const uint32_t nblk = work ? (base + tile_bytes + 63) >> 6 : 0u;
   for (uint32_t blk = tid; blk < nblk; blk += un) {
     uint32_t w[16];
     salsa20_block(w, pre, key.subkey, key.nonce[0], key.nonce[1], b0 + blk);
@@ -436,7 +460,7 @@ __global__ void __launch_bounds__(kBlock)
   // that are still in their keystream loop, so that its LDS and wave slots free up
   if constexpr (MAC) __builtin_amdgcn_s_setprio(3);
   uint8_t* gmsg = ct + (size_t)j * stride + 48;
-  const uint32_t lo = a & ~15u, hi = (a + tile_bytes + 15u) & ~15u, end = a + tile_bytes;
+  const uint32_t lo = a & ~15u, hi = work ? (a + tile_bytes + 15u) & ~15u : 0u, end = a + tile_bytes;
   for (uint32_t c = lo + 16u * tid; c < hi; c += 16u * un) {
     if (c >= a && c + 16u <= end) {
       *reinterpret_cast<uint4*>(gmsg + c) = *reinterpret_cast<const uint4*>(lds + (c - a + base));
@@ -506,6 +530,8 @@ __global__ void __launch_bounds__(kBlock)
       for (int u = 0; u < 5; ++u) atomicAdd(&part[u], (uint32_t)d[u]);
     }
   }
+  if (pass + 1 < kPasses) __syncthreads();  // the next pass overwrites the tile
+  }  // pass
 }
 
 // `err` (may be null): a row whose sum is not `expect` raises kErrMalformed there.
