@@ -703,21 +703,29 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
       Window n0 = {0, 0, 0}, n1 = {0, 0, 0};
       if (t0 != 0) n0 = request(__builtin_ctz(t0));
       if (t1 != 0) n1 = request(__builtin_ctz(t1) + 32);
-      while (__builtin_amdgcn_ballot_w64((t0 | t1) != 0) != 0) {
-        const Window w0 = n0, w1 = n1;
+      // one turn: the windows in (c0, c1) are worked on, the next ones requested into (x0, x1).
+      // Two turns a loop pass with the roles of the two window pairs swapped, so that no
+      // window is copied from "next" to "current" (8 moves a turn otherwise).
+      auto turn = [&](const Window& c0, const Window& c1, Window& x0, Window& x1) {
         const bool h0 = t0 != 0, h1 = t1 != 0;
         t0 &= t0 - 1;
         t1 &= t1 - 1;
-        if (t0 != 0) n0 = request(__builtin_ctz(t0));
-        if (t1 != 0) n1 = request(__builtin_ctz(t1) + 32);
+        if (t0 != 0) x0 = request(__builtin_ctz(t0));
+        if (t1 != 0) x1 = request(__builtin_ctz(t1) + 32);
         if (h0) {
-          emit(w0, a40);
+          emit(c0, a40);
           a40 += 4u;
         }
         if (h1) {
-          emit(w1, a41);
+          emit(c1, a41);
           a41 += 4u;
         }
+      };
+      Window m0 = {0, 0, 0}, m1 = {0, 0, 0};
+      while (__builtin_amdgcn_ballot_w64((t0 | t1) != 0) != 0) {
+        turn(n0, n1, m0, m1);
+        if (__builtin_amdgcn_ballot_w64((t0 | t1) != 0) == 0) break;
+        turn(m0, m1, n0, n1);
       }
       rank += total;
     }
