@@ -1125,7 +1125,21 @@ __global__ void __launch_bounds__(kBlock)
   if (j >= M) return;  // wave-uniform
   const MsgKey key = keys[j];
   const uint32_t rk[4] = {key.poly_r[0], key.poly_r[1], key.poly_r[2], key.poly_r[3]};
-  const P130 f = p130_carry(p130_pow(p130_r_from_key(rk), (uint32_t)lane + 1u));
+  // r^(lane + 1) as a running product over the lanes: six multiplies by the value 1, 2, 4, ...
+  // lanes below (the lanes without one multiply by 1) instead of a square-and-multiply per
+  // lane, which costs the wave all twelve of its steps
+  P130 f = p130_r_from_key(rk);
+#pragma unroll
+  for (int sft = 1; sft < 64; sft <<= 1) {
+    P130 y;
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      const uint32_t up = (uint32_t)__shfl_up((int)f.v[u], sft, 64);
+      y.v[u] = lane >= sft ? up : (u == 0 ? 1u : 0u);
+    }
+    f = p130_mul(f, y);
+  }
+  f = p130_carry(f);
   uint32_t* out = pows + (size_t)j * kPowShortWords + lane * 5;
 #pragma unroll
   for (int u = 0; u < 5; ++u) out[u] = f.v[u];
