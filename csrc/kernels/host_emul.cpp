@@ -10,6 +10,7 @@
 
 #include "decode_core.hpp"
 #include "device_crypto.hpp"
+#include "encode_units.hpp"
 #include "kernels.hpp"
 #include "modarith.hpp"
 #include "sda/crypto.hpp"
@@ -749,6 +750,50 @@ int main() {
       }
     }
     CHECK(ok, "varint_pair16 against zigzag LEB128");
+  }
+  // 9. the encode kernel's work units: every tile of every message exactly once, ends
+  // together only where they are short, no unit outside the launch's grid
+  {
+    const int Ls[] = {1, 7, 2047, 2048, 2049, 8191, 8192, 8193, 10000, 10240, 16382, 25000,
+                      65536, 65537, 70000, 150001};
+    const int Ms[] = {1, 3, 4, 5, 64, 1000};
+    for (int mac = 0; mac < 2; ++mac)
+      for (int L : Ls)
+        for (int M : Ms) {
+          const int tiles = (L + kEncodeValues - 1) / kEncodeValues;
+          std::vector<int> seen((size_t)tiles * M, 0);
+          const unsigned grid = encode_grid(mac != 0, M, L);
+          bool ok = true;
+          for (unsigned b = 0; b < grid; ++b) {
+            const EncodeUnit u0 = encode_unit(mac != 0, M, L, (int)b, 0);
+            for (int w = 0; w < (u0.ends ? kWaves : 1); ++w) {
+              const EncodeUnit u = encode_unit(mac != 0, M, L, (int)b, w);
+              ok = ok && u.ends == u0.ends && u.tile >= 0 && u.tile < tiles && u.msg >= 0 && u.msg < M;
+              if (u.ends) ok = ok && !mac && u.tile == tiles - 1 && L - u.tile * kEncodeValues <= kEncodeValues / kWaves;
+              if (ok && !u.idle) ++seen[(size_t)u.tile * M + u.msg];
+            }
+          }
+          for (int c : seen) ok = ok && c == 1;
+          CHECK(ok, "encode work units");
+        }
+  }
+  // 9b. the decode + sum kernels' workgroup order is a permutation of the grid
+  {
+    const unsigned dims[][3] = {{1, 1, 1}, {2, 728, 26}, {2, 19682, 1}, {3, 5, 7}, {7, 1, 1}, {8, 3, 2}, {163, 3, 26}};
+    for (const auto& d : dims) {
+      std::vector<int> seen((size_t)d[0] * d[1] * d[2], 0);
+      bool ok = true;
+      for (unsigned z = 0; z < d[2]; ++z)
+        for (unsigned y = 0; y < d[1]; ++y)
+          for (unsigned x = 0; x < d[0]; ++x) {
+            const SumTileId id = sum_tile_of(d[0], d[1], d[2], x, y, z);
+            ok = ok && id.t >= 0 && (unsigned)id.t < d[0] && id.r >= 0 && (unsigned)id.r < d[1] && id.g >= 0 &&
+                 (unsigned)id.g < d[2];
+            if (ok) ++seen[((size_t)id.g * d[1] + id.r) * d[0] + id.t];
+          }
+      for (int c : seen) ok = ok && c == 1;
+      CHECK(ok, "decode + sum workgroup order");
+    }
   }
   std::printf(failures ? "host_emul: %d FAILURES\n" : "host_emul: all ok\n", failures);
   return failures ? 1 : 0;

@@ -16,6 +16,7 @@
 #include "block_utils.hpp"
 #include "decode_core.hpp"
 #include "device_crypto.hpp"
+#include "encode_units.hpp"
 #include "kernels.hpp"
 #include "modarith.hpp"
 
@@ -150,15 +151,8 @@ __global__ void __launch_bounds__(kBlock)
 // 3,856 -- every first tile went to the even XCDs and every second one to the odd ones, which
 // then waited for the even ones to finish. With fewer than 8 tiles a row the tile index
 // therefore runs slowest: all the rows' first tiles, then all their second ones.
-struct SumTileId {
-  int t, r, g;
-};
 SDA_DEV SumTileId sum_tile_id() {
-  const unsigned T = gridDim.x, R = gridDim.y, G = gridDim.z;
-  if (T >= 8u || (uint64_t)T * R * G >= (1ull << 31)) return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
-  const unsigned n = blockIdx.x + T * (blockIdx.y + R * blockIdx.z), RG = R * G;
-  const unsigned t = n / RG, rest = n - t * RG, g = rest / R;
-  return {(int)t, (int)(rest - g * R), (int)g};
+  return sum_tile_of(gridDim.x, gridDim.y, gridDim.z, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // Each wave walks its own participants (round-robin over the group) in 4 KiB

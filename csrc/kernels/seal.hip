@@ -17,6 +17,7 @@
 // per-message pass chains the chunk partials with r^(C/16).
 #include "block_utils.hpp"
 #include "device_crypto.hpp"
+#include "encode_units.hpp"
 #include "kernels.hpp"
 #include "modarith.hpp"
 
@@ -98,20 +99,6 @@ SDA_DEV void load_values(uint32_t (&v)[kValuesPerLane], const VT* src, int e0, i
 // i.e. six / four / three workgroups a CU; the issue-bound kernel ran at 57 % of its
 // VALU peak with three -- and a value past the bound (a caller's error: the slots of
 // the arena are sized by the same bound) is encoded as zero rather than overrun it.
-// Whether the messages' ends (the values behind their last whole tile) go four to a workgroup,
-// and the grid that follows from it: whole tiles first, then the ends.
-template <bool MAC>
-__host__ __device__ inline bool encode_short_ends(int L) {
-  const int r = L % kEncodeValues;
-  return !MAC && r > 0 && r <= kEncodeValues / kWaves;
-}
-template <bool MAC>
-static unsigned encode_grid(int M, int L) {
-  const unsigned whole = (unsigned)(L / kEncodeValues) * (unsigned)M;
-  if (L % kEncodeValues == 0) return whole;
-  return whole + (encode_short_ends<MAC>(L) ? (unsigned)(M + kWaves - 1) / kWaves : (unsigned)M);
-}
-
 template <typename VT, bool MAC, int kMaxB>
 __global__ void __launch_bounds__(kBlock)
     k_encode_encrypt(int L, int M, const VT* __restrict__ vals, const uint32_t* __restrict__ tile_off,
@@ -141,9 +128,9 @@ __global__ void __launch_bounds__(kBlock)
   }
   const int T = (L + kTileValues - 1) / kTileValues;  // count tiles per message
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  // Workgroup -> (tile, message): first every message's whole tiles, the message index running
-  // fastest where messages are short, then the ends (encode_grid). Workgroups go round-robin over the 8 XCDs; with
-  // the tile index fastest, messages of two tiles -- a whole one and a short end, the boxes of
+  // Workgroup -> (tile, message): first every message's whole tiles, then the ends
+  // (encode_units.hpp). Workgroups go round-robin over the 8 XCDs; with the tile index fastest
+  // in the grid, messages of two tiles -- a whole one and a short end, the boxes of
   // the many-clerk rounds -- sent every whole tile to the even XCDs and every end to the odd
   // ones, which then stood idle: the kernel took as long as half the chip needs for the whole
   // tiles (3.0 ps a value for boxes of 10,000 values, 2.2 for boxes of ten whole tiles).
@@ -151,23 +138,9 @@ __global__ void __launch_bounds__(kBlock)
   // the ends of four messages, a wave each, instead of keeping an LDS tile and four wave slots
   // busy with one or two waves at work (another 6 %: 2.45 -> 2.30 ps). `un` threads numbered
   // `tid` work on one tile: the workgroup's 256, or a wave's 64.
-  const int whole = L / kEncodeValues, b = blockIdx.x;
-  const bool ends = b >= whole * M && encode_short_ends<MAC>(L);  // block-uniform
-  int t, jw;
-  if (b < whole * M) {
-    if (whole < 8) {  // few tiles a message: the message index runs fastest
-      t = b / M;
-      jw = b - t * M;
-    } else {  // long messages: tile by tile (4 % faster there: neighbours in time are neighbours in memory)
-      jw = b / whole;
-      t = b - jw * whole;
-    }
-  } else {
-    t = whole;
-    jw = ends ? kWaves * (b - whole * M) + wave : b - whole * M;
-  }
-  const bool idle = jw >= M;  // a wave without a message: no values, stores nothing
-  const int j = idle ? M - 1 : jw;
+  const EncodeUnit unit = encode_unit(MAC, M, L, (int)blockIdx.x, wave);
+  const bool ends = unit.ends, idle = unit.idle;  // block-uniform; a wave without a message: no values, stores nothing
+  const int t = unit.tile, j = unit.msg;
   const int tid = ends ? lane : (int)threadIdx.x;
   const int un = ends ? 64 : kBlock;
   uint8_t* lds = ends ? tile + (wave % kPassWaves) * kWaveBytes : tile;
@@ -1251,10 +1224,10 @@ static void launch_encode_t(int M, int L, const void* vals, const uint32_t* tile
                             const MsgKey* keys, uint8_t* ct, uint64_t stride, const uint32_t* pows,
                             const uint32_t* pt_len, uint32_t* partials, int K, hipStream_t s) {
   if (pows && pt_len && partials)
-    hipLaunchKernelGGL((k_encode_encrypt<VT, true, (sizeof(VT) > 2 ? 5 : 3)>), dim3(encode_grid<true>(M, L)),
+    hipLaunchKernelGGL((k_encode_encrypt<VT, true, (sizeof(VT) > 2 ? 5 : 3)>), dim3(encode_grid(true, M, L)),
                        dim3(kBlock), 0, s, L, M, (const VT*)vals, tile_off, keys, ct, stride, pows, pt_len, partials, K);
   else
-    hipLaunchKernelGGL((k_encode_encrypt<VT, false, kMaxB>), dim3(encode_grid<false>(M, L)), dim3(kBlock), 0, s, L,
+    hipLaunchKernelGGL((k_encode_encrypt<VT, false, kMaxB>), dim3(encode_grid(false, M, L)), dim3(kBlock), 0, s, L,
                        M, (const VT*)vals,
                        tile_off, keys, ct, stride, pows, pt_len, partials, K);
 }
