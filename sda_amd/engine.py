@@ -44,8 +44,10 @@ class AggregationError(RuntimeError):
 _SIDE_STREAMS: dict = {}
 
 
-def concurrent_stream(device, tries: int = 12, spin_us: int = 250) -> "torch.cuda.Stream":
-    """A stream whose kernels really run beside the current stream's.
+def concurrent_stream(device, tries: int = 12, spin_us: int = 250, slot: str = "side",
+                      beside: Sequence["torch.cuda.Stream"] = ()) -> "torch.cuda.Stream":
+    """A stream whose kernels really run beside the current stream's (and beside
+    those of the streams in `beside`); one per current stream and `slot`.
 
     HIP multiplexes a process's streams onto few hardware queues (4 by default),
     and two streams on one queue serialise -- which of them share a queue
@@ -57,7 +59,7 @@ def concurrent_stream(device, tries: int = 12, spin_us: int = 250) -> "torch.cud
     queue. Falls back to the last candidate (correct, only slower)."""
     dev = torch.device(device)
     main = torch.cuda.current_stream(dev)
-    key = (dev.index, main.cuda_stream)
+    key = (dev.index, main.cuda_stream, slot)
     if key in _SIDE_STREAMS:
         return _SIDE_STREAMS[key]
     gate = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -69,6 +71,9 @@ def concurrent_stream(device, tries: int = 12, spin_us: int = 250) -> "torch.cud
             torch.cuda.synchronize(dev)
             e0.record(main)
             G.gate_wait((gate, 1), timeout_us=spin_us)  # main: never posted, ends at the limit
+            for other in beside:
+                with torch.cuda.stream(other):
+                    G.gate_wait((gate, 1), timeout_us=spin_us)
             with torch.cuda.stream(cand):
                 G.gate_wait((gate, 0), timeout_us=1)    # candidate: returns at once
                 e1.record(cand)
@@ -135,15 +140,51 @@ class KeyTable:
         return cls(pks, sks, pk, sk)
 
 
-@dataclass
 class RoundResult:
-    output: torch.Tensor          # int32 [D], canonical in [0, m)
-    clerks_used: list
-    stage_ms: dict
-    # the round's device error word (int32 [1]; see describe_error). Already
-    # read and raised on when the round ran with check=True; callers that time
-    # unchecked rounds OR these together and read the result once.
-    err: Optional[torch.Tensor] = None
+    """What a round returns: `output` (int32 [D], canonical in [0, m); None on the
+    ranks of a reduced round that do not reveal), `clerks_used`, `stage_ms`, and
+    `err`, the round's device error word (int32 [1]; see describe_error) -- already
+    read and raised on when the round ran with check=True; callers that time
+    unchecked rounds OR these together and read the result once.
+
+    An unchecked round may have run its recipient stage on a stream of its own
+    (DeviceAggregator.run_round): `output` and `err` then belong to that stream
+    until first read, and reading them makes the *current* stream wait for it.
+    A loop that wants the next round's kernels to start meanwhile reads them one
+    round late."""
+
+    def __init__(self, output, clerks_used, stage_ms, err: Optional[torch.Tensor] = None):
+        self._output, self._err = output, err
+        self.clerks_used, self.stage_ms = clerks_used, stage_ms
+        self._ready = None  # (event, device) while the recipient stage's stream owns the tensors
+
+    def _join(self):
+        if self._ready is not None:
+            ev, dev = self._ready
+            self._ready = None
+            cur = torch.cuda.current_stream(dev)
+            cur.wait_event(ev)
+            for t in (self._output, self._err):
+                if t is not None:
+                    t.record_stream(cur)
+
+    @property
+    def output(self):
+        self._join()
+        return self._output
+
+    @output.setter
+    def output(self, value):
+        self._output = value
+
+    @property
+    def err(self):
+        self._join()
+        return self._err
+
+    @err.setter
+    def err(self, value):
+        self._err = value
 
 
 class DeviceAggregator:
@@ -160,6 +201,8 @@ class DeviceAggregator:
         if isinstance(spec.sharing, PackedShamir) and self.m <= 256 and share_storage != "u16":
             self.vdtype = torch.uint8  # a field element per byte
         self.time_stages = time_stages
+        # unchecked rounds run their result path on a stream of its own (_reveal_beside)
+        self.overlap_reveal = True
         self._round = 0
         if isinstance(spec.sharing, PackedShamir):
             p = spec.sharing.native()
@@ -262,6 +305,14 @@ class DeviceAggregator:
             self._side = concurrent_stream(self.device)
         return self._side
 
+    def _tail_stream(self):
+        if getattr(self, "_tail", None) is None:
+            # beside the main stream and beside the side stream: on the side stream's
+            # queue the next round's key agreement would wait for this round's result
+            # path, and the main stream's first grid waits for that key agreement
+            self._tail = concurrent_stream(self.device, slot="tail", beside=[self._side_stream()])
+        return self._tail
+
     def _live(self, clerks):
         spec, n = self.spec, self.n
         live = list(range(n)) if clerks is None else sorted(set(int(c) for c in clerks))
@@ -340,6 +391,13 @@ class DeviceAggregator:
         self._mark(marks, "start")
         combined, mask_sum = self.participate_and_clerk(secrets, live, err, owner_base=owner_base,
                                                         marks=marks)
+        main = torch.cuda.current_stream(self.device)
+        if self.overlap_reveal and reducer is None and not check and not self.time_stages:
+            return self._reveal_beside(main, combined, mask_sum, live, err)
+        if getattr(self, "_tail_ev", None) is not None:
+            # an earlier round's recipient stage ran on the tail stream: whatever it
+            # created there for later rounds (cached matrices) is ordered before this one
+            main.wait_event(self._tail_ev)
         # the recipient's key agreement queues on the side stream BEHIND the
         # participants' and clerks' (needed last; ahead of them it delayed the
         # first encrypt by the length of an X25519 ladder)
@@ -350,6 +408,28 @@ class DeviceAggregator:
                 return self._finish(err, marks, check, RoundResult(None, live, {}))
         out = self.reveal(combined, mask_sum, live, err, marks=marks, keys=rk)
         return self._finish(err, marks, check, RoundResult(out, live, {}))
+
+    def _reveal_beside(self, main, combined, mask_sum, live, err) -> RoundResult:
+        """The result path of an unchecked round -- clerks seal their sums, the
+        recipient opens, reconstructs and unmasks -- on a third stream. It is a
+        chain of ~15 dependent launches over a handful of boxes, 0.2 ms during
+        which the card is nearly idle; on the main stream the next round's first
+        grid waited for it. The result's tensors belong to that stream until
+        first read (RoundResult)."""
+        tail = self._tail_stream()
+        tail.wait_stream(main)
+        for t in (combined, mask_sum, err):  # main-stream tensors used on the tail
+            if t is not None:
+                t.record_stream(tail)
+        with torch.cuda.stream(tail):
+            rk = self.prepare_reveal(live, err)
+            out = self.reveal(combined, mask_sum, live, err, keys=rk)
+            result = self._finish(err, [], False, RoundResult(out, live, {}))
+            ev = torch.cuda.Event()
+            ev.record(tail)
+        result._ready = (ev, self.device)
+        self._tail_ev = ev
+        return result
 
     def participate_and_clerk(self, secrets: torch.Tensor, live, err, owner_base: int = 0,
                               marks=None):

@@ -55,8 +55,9 @@ class DistributedAggregator:
     :class:`sda_amd.host_engine.HostAggregator` (CPU; gloo tests).
 
     `deadline_s` bounds the wait for clerk results; `fault_hook(stage, rank)`
-    is called at the stage boundaries ("before_partials", "before_results") --
-    the fault-injection point of the tests.
+    is called at the stage boundaries ("before_partials", "before_results") and,
+    on the host engines, between the result rendezvous and the transfer it
+    decided ("before_result_transfer") -- the fault-injection points of the tests.
     """
 
     def __init__(self, spec: AggregationSpec, engine: str = "device", device=None, group=None,
@@ -321,6 +322,9 @@ class DistributedAggregator:
             sealed[c] = eng.seal_result(tot)
         self._hook("before_results")
         arrived = result_stage(comm, topic, live, n, ft, sealed, ROOT)
+        # (a rank lost from here on has already been counted in: the recipient's
+        # receive from it fails when the backend notices, not at the rendezvous)
+        self._hook("before_result_transfer")
         need = spec.sharing.reconstruction_threshold()
         enough = len(arrived) >= need
         res_in = torch.zeros(len(live), stride, dtype=torch.uint8) if me == ROOT else None

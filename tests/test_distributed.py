@@ -217,6 +217,24 @@ def test_host_of_a_spanning_clerk_dies(native, stage):
     assert sorted(r[1] for r in results if r[0] == "ok") == [2, 3]
 
 
+def test_clerk_rank_dies_between_the_rendezvous_and_its_transfer(native):
+    """The window the rendezvous cannot close: rank 5 posts its result flag, is
+    counted in by the recipient, and exits before its sealed result has left.
+    The recipient's receive from it must fail -- a raised error and a process
+    that ends, not a hang -- and ranks that have nothing to do with rank 5
+    finish their round."""
+    import time
+
+    t0 = time.monotonic()
+    results = _run(8, "pss", P=2, D=10, die=(5,), die_stage="before_result_transfer")
+    assert time.monotonic() - t0 < 110  # below the workers' 120 s process-group timeout
+    assert ("died", 5) in results
+    raised = [r for r in results if r[0] == "raised"]
+    assert [r[1] for r in raised] == [0], results
+    assert "Not enough clerk results" not in raised[0][2]  # a transport error, not a decision
+    assert sorted(r[1] for r in results if r[0] == "ok") == [1, 2, 3, 4, 6, 7]
+
+
 def test_host_engine_single_process(native):
     from sda_amd.host_engine import HostAggregator
 
