@@ -303,6 +303,7 @@ def main():
         comm.reset_audit()
         comm.barrier()
     err_total.zero_()
+    engine.take_errors()  # the warm-up's words: checked already
     torch.cuda.synchronize()
     torch.cuda.reset_peak_memory_stats()
     res = None
@@ -316,9 +317,12 @@ def main():
         th = time.perf_counter()
         res = agg.run_round(secrets, check=args.check)
         host_s += time.perf_counter() - th
-        err_total |= res.err  # device-side OR: read once, after the clock stops
         if args.check:
             verify(res, f"step {i}")
+    # the error words of the timed rounds are OR-ed on the device by the engine (on the
+    # stream each round's result path ends on, beside the next round's first kernels)
+    # and read once, after the clock stops
+    err_total |= engine.take_errors()
     torch.cuda.synchronize()
     if dist_mode:
         comm.barrier()

@@ -213,9 +213,10 @@ def gpu_configs(args):
         err_total.zero_()
         sync()
         t0 = time.perf_counter()
+        eng.take_errors()
         for _ in range(args.steps):
-            res = step(False)        # no host synchronisation inside the timed loop:
-            err_total |= res.err     # the error words are OR-ed on the device, read once
+            res = step(False)        # no host synchronisation inside the timed loop: the
+        err_total |= eng.take_errors()  # engine ORs the rounds' error words on the device
         sync()
         secs = time.perf_counter() - t0
         e = int(err_total.item())

@@ -40,6 +40,12 @@ def native():
 
 def gpu():
     """The gfx950 kernel module. Raises loudly if it is missing."""
+    if "_sda_gpu" not in _cache:
+        # torch first: it brings its own copy of the HIP runtime, and the module must
+        # bind to the runtime torch's streams and tensors belong to. Loaded ahead of
+        # torch, the module pulled in the system's runtime and its first launch failed
+        # with "no ROCm-capable device is detected" once torch had initialised its own.
+        import torch  # noqa: F401
     return _load("_sda_gpu")
 
 

@@ -67,13 +67,23 @@ def concurrent_stream(device, tries: int = 12, spin_us: int = 250, slot: str = "
     with torch.cuda.device(dev):
         for _ in range(tries):
             cand = torch.cuda.Stream(device=dev)
+            with torch.cuda.stream(cand):
+                # a stream's first launch attaches it to its hardware queue, which takes
+                # longer than the spin below: measured cold, every candidate looked late
+                G.gate_wait((gate, 0), timeout_us=1)
             e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
             torch.cuda.synchronize(dev)
             e0.record(main)
             G.gate_wait((gate, 1), timeout_us=spin_us)  # main: never posted, ends at the limit
-            for other in beside:
-                with torch.cuda.stream(other):
-                    G.gate_wait((gate, 1), timeout_us=spin_us)
+            if beside:
+                # a wait for the end of that spin queued on each of them: a stream's wait
+                # holds up everything behind it in its hardware queue, other streams'
+                # kernels included (seen in a kernel trace: key agreement submitted on
+                # one stream stood behind the result path's wait for the main stream)
+                spun = torch.cuda.Event()
+                spun.record(main)
+                for other in beside:
+                    other.wait_event(spun)
             with torch.cuda.stream(cand):
                 G.gate_wait((gate, 0), timeout_us=1)    # candidate: returns at once
                 e1.record(cand)
@@ -201,7 +211,7 @@ class DeviceAggregator:
         if isinstance(spec.sharing, PackedShamir) and self.m <= 256 and share_storage != "u16":
             self.vdtype = torch.uint8  # a field element per byte
         self.time_stages = time_stages
-        # unchecked rounds run their result path on a stream of its own (_reveal_beside)
+        # rounds run their result path on a stream of its own (_reveal_beside)
         self.overlap_reveal = True
         self._round = 0
         if isinstance(spec.sharing, PackedShamir):
@@ -392,8 +402,15 @@ class DeviceAggregator:
         combined, mask_sum = self.participate_and_clerk(secrets, live, err, owner_base=owner_base,
                                                         marks=marks)
         main = torch.cuda.current_stream(self.device)
-        if self.overlap_reveal and reducer is None and not check and not self.time_stages:
-            return self._reveal_beside(main, combined, mask_sum, live, err)
+        if self.overlap_reveal and reducer is None and not self.time_stages:
+            # checked rounds too: the same path (and the same stream's memory pool)
+            # whether or not the caller reads the result at once
+            result = self._reveal_beside(main, combined, mask_sum, live, err)
+            if check:
+                e = int(result.err.item())  # joins the tail stream, then the host
+                if e:
+                    raise AggregationError(f"device error word 0x{e:x} ({describe_error(e)})")
+            return result
         if getattr(self, "_tail_ev", None) is not None:
             # an earlier round's recipient stage ran on the tail stream: whatever it
             # created there for later rounds (cached matrices) is ordered before this one
@@ -410,19 +427,22 @@ class DeviceAggregator:
         return self._finish(err, marks, check, RoundResult(out, live, {}))
 
     def _reveal_beside(self, main, combined, mask_sum, live, err) -> RoundResult:
-        """The result path of an unchecked round -- clerks seal their sums, the
-        recipient opens, reconstructs and unmasks -- on a third stream. It is a
+        """The result path of a round -- clerks seal their sums, the recipient
+        opens, reconstructs and unmasks -- on a third stream. It is a
         chain of ~15 dependent launches over a handful of boxes, 0.2 ms during
         which the card is nearly idle; on the main stream the next round's first
         grid waited for it. The result's tensors belong to that stream until
         first read (RoundResult)."""
         tail = self._tail_stream()
+        # the recipient's key agreement is queued on the side stream first: should the
+        # tail stream share its hardware queue after all, the wait below must not stand
+        # in front of it
+        rk = self.prepare_reveal(live, err)
         tail.wait_stream(main)
-        for t in (combined, mask_sum, err):  # main-stream tensors used on the tail
-            if t is not None:
+        for t in (combined, mask_sum, err, rk[0].ct, rk[0].pt_len, rk[1], rk[2]):
+            if t is not None:  # tensors of the main and side streams used on the tail
                 t.record_stream(tail)
         with torch.cuda.stream(tail):
-            rk = self.prepare_reveal(live, err)
             out = self.reveal(combined, mask_sum, live, err, keys=rk)
             result = self._finish(err, [], False, RoundResult(out, live, {}))
             ev = torch.cuda.Event()
@@ -704,6 +724,12 @@ class DeviceAggregator:
 
     def _finish(self, err, marks, check, result: RoundResult) -> RoundResult:
         result.err = err
+        # the round's error word into the running OR of the stream it ends on
+        acc = self.__dict__.setdefault("_err_acc", {})
+        cur = torch.cuda.current_stream(self.device)
+        if cur.cuda_stream not in acc:
+            acc[cur.cuda_stream] = (torch.zeros_like(err), cur)
+        acc[cur.cuda_stream][0].bitwise_or_(err)
         self.throttle()
         if check or self.time_stages:
             e = int(err.item())
@@ -712,6 +738,21 @@ class DeviceAggregator:
             for (a, ea), (b, eb) in zip(marks, marks[1:]):
                 result.stage_ms[b] = ea.elapsed_time(eb)
         return result
+
+    def take_errors(self) -> torch.Tensor:
+        """The OR of the error words of every round since the last call (int32 [1], on
+        the current stream; see describe_error), and a fresh start. A loop of
+        unchecked rounds reads this once at its end instead of a word per round:
+        reading a round's own word orders the reader behind that round's result
+        path, which otherwise runs beside the next round's first kernels."""
+        cur = torch.cuda.current_stream(self.device)
+        total = self.new_error_word()
+        for word, stream in self.__dict__.pop("_err_acc", {}).values():
+            if stream != cur:
+                cur.wait_stream(stream)
+                word.record_stream(cur)
+            total |= word
+        return total
 
     def _lagrange_limbs(self, live):
         key = ("limbs",) + tuple(live)

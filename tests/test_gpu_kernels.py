@@ -574,6 +574,66 @@ def test_unchecked_rounds_stay_two_deep(cuda):
         assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("name", ["additive", "fullmask", "chachamask", "pss", "pss_dropout"])
+def test_unchecked_rounds_result_path_beside_the_next_round(cuda, name):
+    """Unchecked rounds run their result path (clerks seal, recipient opens,
+    reconstructs, unmasks) on a stream of their own and hand the tensors over at
+    first read. Rounds over different inputs, read one round late (as the
+    benchmarks do), read at once, and mixed with checked rounds, all give the
+    plain sums; the overlap can be switched off and changes nothing."""
+    from sda_amd.engine import DeviceAggregator, reference_sum
+    from sda_amd.models import (PSS_4_8_3, Additive, AggregationSpec, ChaChaMask, FullMask,
+                                pss_5_of_8)
+    D, P, m = 30011, 12, 433
+    clerks = None
+    if name == "additive":
+        spec = AggregationSpec(D, m, Additive(3, m))
+    elif name == "fullmask":
+        spec = AggregationSpec(D, m, Additive(3, m), FullMask(m))
+    elif name == "chachamask":
+        spec = AggregationSpec(D, m, Additive(3, m), ChaChaMask(m, D))
+    elif name == "pss":
+        spec = AggregationSpec(D, m, PSS_4_8_3)
+    else:
+        spec, clerks = AggregationSpec(D, m, pss_5_of_8()), [0, 2, 3, 5, 7]
+    agg = DeviceAggregator(spec, cuda)
+    xs = [torch.randint(0, m, (P, D), dtype=torch.int32, device=cuda) for _ in range(6)]
+    refs = [reference_sum(x, m) for x in xs]
+    # read one round late
+    prev, got = None, []
+    for x in xs:
+        res = agg.run_round(x, clerks=clerks, check=False)
+        assert res._ready is not None  # its result path went to the tail stream
+        if prev is not None:
+            got.append((prev.output, prev.err))
+        prev = res
+    got.append((prev.output, prev.err))
+    assert prev._ready is None
+    # a checked round right behind unchecked ones, then unchecked ones read at once
+    chk = agg.run_round(xs[0], clerks=clerks)
+    assert chk._ready is None and torch.equal(chk.output, refs[0])  # joined by its own check
+    now = [agg.run_round(x, clerks=clerks, check=False).output.clone() for x in xs[:3]]
+    agg.overlap_reveal = False
+    off = agg.run_round(xs[1], clerks=clerks, check=False)
+    assert off._ready is None
+    torch.cuda.synchronize()
+    for (out, err), ref in zip(got, refs):
+        assert int(err.item()) == 0
+        assert torch.equal(out, ref)
+    for out, ref in zip(now, refs):
+        assert torch.equal(out, ref)
+    assert int(off.err.item()) == 0 and torch.equal(off.output, refs[1])
+    # the engine's running OR over all of these rounds, and a round that must raise it
+    assert int(agg.take_errors().item()) == 0
+    agg.overlap_reveal = True
+    agg.run_round(xs[2], clerks=clerks, check=False)
+    agg.corrupt_next_round()
+    agg.run_round(xs[3], clerks=clerks, check=False)
+    agg.run_round(xs[4], clerks=clerks, check=False)
+    assert int(agg.take_errors().item()) != 0
+    assert int(agg.take_errors().item()) == 0  # taken: a fresh start
+
+
 def test_round_additive(cuda):
     from sda_amd.models import AggregationSpec, Additive
     _round(cuda, AggregationSpec(10000, 433, Additive(3, 433)), 7)
