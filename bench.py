@@ -292,11 +292,22 @@ def main():
     # the timed loop too: the first use of an op in a process loads its code object,
     # which on a machine that has not run the program before reads it from disk
     # (tens of ms, measured: a first process timed 17 ms rounds, every later one 13.6)
+    # They are queued the way the timed rounds are -- unchecked, two in flight -- and
+    # checked afterwards: a second round in flight needs a second set of arenas, and
+    # rounds that are read back one by one left that allocation to the timed loop.
     err_total = torch.zeros(1, dtype=torch.int32, device="cuda")
-    for i in range(args.warmup):
-        res = agg.run_round(secrets, check=True)
+    warm = [agg.run_round(secrets, check=False) for _ in range(args.warmup)]
+    for i, res in enumerate(warm):
         err_total |= res.err
+        e = int(res.err.item())
+        if dist_mode:
+            e = comm.all_reduce_or(e)
+        if e:
+            from sda_amd.engine import describe_error
+
+            raise SystemExit(f"bench: warmup round {i}: device error word 0x{e:x} ({describe_error(e)})")
         verify(res, f"warmup round {i}")
+    del warm
     if args.warmup == 0:
         err_total |= err_total
     if dist_mode:

@@ -210,10 +210,14 @@ def gpu_configs(args):
             tot = agg.comm.reduce_sum(local_sum) if world > 1 else local_sum
             if rank == 0:
                 ok = bool(torch.equal(res.output, torch.remainder(tot, m).to(torch.int32)))
+        # ... and unchecked ones, queued two deep like the timed rounds: the second round
+        # in flight needs its own set of arenas, allocated here and not in the timed loop
+        for _ in range(3 if args.steps > 1 else 0):
+            step(False)
         err_total.zero_()
+        err_total |= eng.take_errors()  # (the warm-up's words count too)
         sync()
         t0 = time.perf_counter()
-        eng.take_errors()
         for _ in range(args.steps):
             res = step(False)        # no host synchronisation inside the timed loop: the
         err_total |= eng.take_errors()  # engine ORs the rounds' error words on the device
