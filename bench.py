@@ -23,7 +23,7 @@ shares reach rank 0 -- the recipient -- sealed. `--layout owner` is an explicit
 non-private upper bound (each GPU opens its own participants' boxes and the
 plaintext partial sums are reduced): it shows what the all-to-all costs.
 
-Launch: python bench.py --gpus 1 --steps 5 --warmup 2
+Launch: python bench.py                                   (1 GPU, 20 timed rounds after 5)
         python bench.py --gpus N --steps K --warmup W      (starts its own N ranks)
         python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
             --master-port P bench.py --gpus N --steps K --warmup W
@@ -83,8 +83,11 @@ def arx_floor_ms(P: int, D: int, n: int, m: int) -> float:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5,
+                    help="untimed rounds first; fewer than ~4 leave the card's clocks still "
+                         "rising when the clock starts (the first rounds after idling run "
+                         "14.6, 12.8, 12.5 ms)")
     ap.add_argument("--participants", type=int, default=1000, help="participants per rank")
     ap.add_argument("--dim", type=int, default=1_000_000)
     ap.add_argument("--clerks", type=int, default=3)
@@ -288,33 +291,39 @@ def main():
         if rank == 0 and not torch.equal(res.output, expected):
             raise SystemExit(f"bench: {what}: aggregate does not match the reference sum")
 
-    # warmup: checked rounds (device error word + output). They run every device op of
-    # the timed loop too: the first use of an op in a process loads its code object,
-    # which on a machine that has not run the program before reads it from disk
-    # (tens of ms, measured: a first process timed 17 ms rounds, every later one 13.6)
-    # They are queued the way the timed rounds are -- unchecked, two in flight -- and
-    # checked afterwards: a second round in flight needs a second set of arenas, and
-    # rounds that are read back one by one left that allocation to the timed loop.
+    # warmup: rounds queued exactly as the timed ones are -- unchecked, two in flight --
+    # and checked (device error word + output) after the clock has stopped. Three things
+    # are being warmed. The first use of an op in a process loads its code object, which
+    # on a machine that has not run the program before reads it from disk (tens of ms,
+    # measured: a first process timed 17 ms rounds, every later one 13.6). A second round
+    # in flight needs a second set of arenas, and rounds read back one by one left that
+    # allocation to the timed loop. And the card's clocks: a few milliseconds without
+    # work (the host reading a result back) and the next round takes 14.6 ms instead of
+    # 12.4, the one after it 12.8 (scripts/exp_round_steps.py) -- so nothing is read
+    # back between the last warm-up round and the timed region: the synchronisation
+    # in front of the clock ends with the card still at its working clocks.
     err_total = torch.zeros(1, dtype=torch.int32, device="cuda")
-    warm = [agg.run_round(secrets, check=False) for _ in range(args.warmup)]
-    for i, res in enumerate(warm):
-        err_total |= res.err
-        e = int(res.err.item())
-        if dist_mode:
-            e = comm.all_reduce_or(e)
-        if e:
-            from sda_amd.engine import describe_error
 
-            raise SystemExit(f"bench: warmup round {i}: device error word 0x{e:x} ({describe_error(e)})")
-        verify(res, f"warmup round {i}")
-    del warm
-    if args.warmup == 0:
-        err_total |= err_total
+    def device_verdict(r):
+        # a round's error word and "output differs" as device values, no read-back
+        wrong = (r.output != expected).any() if rank == 0 else None
+        return r.err.clone(), wrong
+
+    warm, prev = [], None
+    for _ in range(args.warmup):
+        r = agg.run_round(secrets, check=False)
+        if prev is not None:  # one round late: reading a result waits for its result path
+            warm.append(device_verdict(prev))
+        prev = r
+    if prev is not None:
+        warm.append(device_verdict(prev))
+    del prev
+    err_total |= err_total  # (the timed region's own ops, used once)
     if dist_mode:
         comm.reset_audit()
         comm.barrier()
     err_total.zero_()
-    engine.take_errors()  # the warm-up's words: checked already
+    engine.take_errors()  # the warm-up's words: each is checked below, after the clock
     torch.cuda.synchronize()
     torch.cuda.reset_peak_memory_stats()
     res = None
@@ -350,6 +359,16 @@ def main():
         raise SystemExit(f"bench: device error word 0x{e:x} in the timed steps ({describe_error(e)})")
     if res is not None:
         verify(res, "last timed round")
+    for i, (w_err, w_wrong) in enumerate(warm):  # the warm-up rounds: each one's verdict
+        e = int(w_err.item())
+        if dist_mode:
+            e = comm.all_reduce_or(e)
+        if e:
+            from sda_amd.engine import describe_error
+
+            raise SystemExit(f"bench: warmup round {i}: device error word 0x{e:x} ({describe_error(e)})")
+        if w_wrong is not None and bool(w_wrong.item()):
+            raise SystemExit(f"bench: warmup round {i}: aggregate does not match the reference sum")
     ms = elapsed / max(1, args.steps) * 1e3
     total_elems = P * world * args.dim
     value = total_elems / (ms / 1e3)
