@@ -122,6 +122,7 @@ clean:
 check: all
 	$(PYTHON) -m pytest tests -x -q -m "not gpu"
 	$(MAKE) asan tsan emul
+	bash docs/cli-walkthrough.sh > /dev/null
 
 # host emulation of the device algorithms (no GPU needed)
 emul: $(BUILD)/hip/host_emul

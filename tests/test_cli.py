@@ -178,3 +178,15 @@ def test_daemon_enforces_body_budget(tmp_path, native):
         except subprocess.TimeoutExpired:
             proc.kill()
             proc.wait()
+
+
+@pytest.mark.parametrize("args", [[], ["--mask", "full", "--sharing", "shamir", "--clerks", "8"]])
+def test_walkthrough_script(native, args):
+    """docs/cli-walkthrough.sh: the reference's docs/simple-cli-example.sh for these
+    binaries, which -- unlike that script -- fails unless the revealed sum is right."""
+    script = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "docs",
+                          "cli-walkthrough.sh")
+    r = subprocess.run(["bash", script, *args], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "values: [0, 2, 2, 4, 4, 6, 6, 8, 8, 10]" in r.stdout
+    assert r.stdout.strip().splitlines()[-1].startswith("walkthrough ok")
