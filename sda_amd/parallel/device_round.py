@@ -73,6 +73,9 @@ class DeviceCommittee:
         self.force_pipeline = force_pipeline
         self.fault_tolerant = fault_tolerant
         self.fault_hook = fault_hook
+        # the clerks' key agreement queued behind the first wave's share kernel (True) or
+        # beside it (False: as early as possible)
+        self.open_keys_behind_share = True
         n, W, me = engine.n, comm.world, comm.rank
         self.hosted = hosted_clerks(me, W, n)
         self.led = [c for c in self.hosted if lead(c, W, n) == me]
@@ -245,25 +248,37 @@ class DeviceCommittee:
                 ks_mask = seal_setup(mask_arena, kidx_rcpt, pks, rng_key, n * P, err).with_powers()
             ev_seal = torch.cuda.Event()
             ev_seal.record(side)
-            # the ephemeral-key headers ahead of the data, then the clerks' open keys
-            if alias:
-                ko = open_setup(arena, kidx_in, sks, pks, err)
-            else:
-                hdr = arena.ct.view(arena.M, arena.stride)[:, :32].contiguous()
-                hdr_in = torch.empty(rows_in, 32, dtype=torch.uint8, device=dev)
-                sends, recvs = [], []
-                for (lo, hi), r, base in zip(bounds, routers, in_base):
-                    s_, r_ = r.ops([(hdr, hdr_in)], src_base=n * lo, dst_base=base, kind="hdr")
-                    sends += s_
-                    recvs += r_
-                h = comm.exchange_async(sends, recvs)
-                h.wait()
-                ko = open_setup(_header_arena(hdr_in, arena.K), kidx_in, sks, pks, err)
-            ev_open = torch.cuda.Event()
-            ev_open.record(side)
+
+        opened = {}
+
+        def open_keys():
+            # The ephemeral-key headers ahead of the data, then the clerks' open keys.
+            # Queued behind the first wave's share kernel, not beside it: beside it the
+            # ladder waves take register space from the share grid (a one-wave round's
+            # share kernel ran 2.96 ms instead of 2.40).
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                if alias:
+                    ko = open_setup(arena, kidx_in, sks, pks, err)
+                else:
+                    hdr = arena.ct.view(arena.M, arena.stride)[:, :32].contiguous()
+                    hdr_in = torch.empty(rows_in, 32, dtype=torch.uint8, device=dev)
+                    sends, recvs = [], []
+                    for (lo, hi), r, base in zip(bounds, routers, in_base):
+                        s_, r_ = r.ops([(hdr, hdr_in)], src_base=n * lo, dst_base=base, kind="hdr")
+                        sends += s_
+                        recvs += r_
+                    h = comm.exchange_async(sends, recvs)
+                    h.wait()
+                    ko = open_setup(_header_arena(hdr_in, arena.K), kidx_in, sks, pks, err)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            ko.record_stream(main)
+            opened["ko"], opened["ev"] = ko, ev
+
         # caching-allocator stream bookkeeping: side-allocated keys are consumed on
         # main, main-allocated buffers are touched on side
-        for t in (ks, ks_mask, ko):
+        for t in (ks, ks_mask):
             if t is not None:
                 t.record_stream(main)
         for t in (arena.ct, kidx_send, kidx_in, kidx_rcpt) + \
@@ -280,7 +295,8 @@ class DeviceCommittee:
 
         def finish(w, handle):
             handle.wait()
-            main.wait_event(ev_open)
+            ko = opened["ko"]
+            main.wait_event(opened["ev"])
             pl, base = plans[w], in_base[w]
             segs = [(i, s) for i, s in enumerate(pl.segments) if s.count and s.clerk in live]
             if not segs:
@@ -309,11 +325,15 @@ class DeviceCommittee:
                              rows=1, out=None, acc=acc[s.clerk])
 
         pending = None
+        if not self.open_keys_behind_share:
+            open_keys()
         G.gate_wait(gate)
         for w, (lo, hi) in enumerate(bounds):
             Pw = hi - lo
             shares, cnt, mvals, mcnt = eng._share(secrets[lo:hi], rng_key, owner_base + lo, err)
             if w == 0:  # the first wave's shares overlap the whole-round seal setup
+                if self.open_keys_behind_share:
+                    open_keys()
                 main.wait_event(ev_seal)
             box = arena.slice(n * lo, n * Pw)
             seal_data(box, ks.slice(n * lo, n * Pw), shares.view(n * Pw, B), err, cnt)
