@@ -433,8 +433,14 @@ def main():
             "pipeline_waves": waves if dist_mode else None,
             "compute_stream_vs_rccl": comm.compute_stream_probe if dist_mode else None,
             "pipeline_wave_tuning_ms": {str(k): v for k, v in wave_tuning.items()} or None,
-            "timed_steps_verified": "device error word of every timed step (OR over steps and "
-                                    "ranks) + last round's output vs the plain sum",
+            "timed_steps_verified": "device error word of every timed step (OR-ed on the device by "
+                                    "the engine over steps, and over ranks) + last round's output vs "
+                                    "the plain sum; every warm-up round's error word and output too, "
+                                    "read after the clock stopped",
+            "round_pipelining": (None if dist_mode else
+                                 "each round complete; a round's result path (clerks seal their "
+                                 "sums, recipient opens + reconstructs) runs on a third stream "
+                                 "beside the next round's first kernels; at most two rounds in flight"),
             "config": {
                 "model": f"SDA round: additive-{args.clerks} sharing, mod {args.modulus}, no mask, "
                          "libsodium sealed boxes (X25519+XSalsa20-Poly1305), zigzag varint",
