@@ -73,6 +73,12 @@ class DeviceCommittee:
         self.force_pipeline = force_pipeline
         self.fault_tolerant = fault_tolerant
         self.fault_hook = fault_hook
+        # Liveness flags say "my host reached this stage"; with strict_liveness they say
+        # "my GPU finished the work in front of this stage": the host waits for its stream
+        # before it posts, so a rank that dies while that work is still running is left
+        # out by its peers instead of being waited for. Costs the host its lead over the
+        # GPU once per guarded stage (rounds no longer queue ahead); off by default.
+        self.strict_liveness = False
         # the clerks' key agreement queued behind the first wave's share kernel (True) or
         # beside it (False: as early as possible)
         self.open_keys_behind_share = True
@@ -405,6 +411,8 @@ class DeviceCommittee:
 
         # ---- clerk-internal: co-hosts' partial sums -> the clerk's lead
         self._hook("before_partials")
+        if ft and self.strict_liveness:
+            torch.cuda.current_stream(dev).synchronize()
         complete, go = partial_stage(comm, topic, live, n, ft)
         sends, recvs, inbound = [], [], {}
         for c in live:
@@ -443,6 +451,8 @@ class DeviceCommittee:
                     combined[ctx.led.index(c)] = torch.remainder(tot, m).to(torch.int32)
             eng.seal_results(ctx.res_arena, ctx.ks_res, combined, err)
         self._hook("before_results")
+        if ft and self.strict_liveness:
+            torch.cuda.current_stream(dev).synchronize()
         arrived = result_stage(comm, topic, live, n, ft, led_ok, root)
         need = eng.spec.sharing.reconstruction_threshold()
         enough = len(arrived) >= need

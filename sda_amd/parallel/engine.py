@@ -58,12 +58,15 @@ class DistributedAggregator:
     is called at the stage boundaries ("before_partials", "before_results") and,
     on the host engines, between the result rendezvous and the transfer it
     decided ("before_result_transfer") -- the fault-injection points of the tests.
+    `strict_liveness` (device engine): a rank posts its liveness flags only once its
+    GPU has finished the work in front of the stage (see DeviceCommittee).
     """
 
     def __init__(self, spec: AggregationSpec, engine: str = "device", device=None, group=None,
                  time_stages: bool = False, layout: str = "committee", waves: int = 4,
                  force_pipeline: bool = False, fault_tolerant: bool = True,
                  deadline_s: float = 60.0, fault_hook=None, pss_backend: str = "auto",
+                 strict_liveness: bool = False,
                  loopback: bool = False, max_op_bytes: int = 1 << 30):
         if layout not in ("committee", "owner"):
             raise ValueError("layout must be 'committee' or 'owner'")
@@ -103,6 +106,7 @@ class DistributedAggregator:
                                                   force_pipeline=force_pipeline,
                                                   fault_tolerant=fault_tolerant,
                                                   fault_hook=fault_hook)
+                self._committee.strict_liveness = strict_liveness
         else:
             from ..host_engine import HostAggregator, HostKeys
 

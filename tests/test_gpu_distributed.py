@@ -41,7 +41,8 @@ def _worker(rank, world, port, name, layout, q):
                 "pss": AggregationSpec(D, m, PSS_4_8_3)}[name]
         agg = DistributedAggregator(spec, engine="device", device=torch.device("cuda", 0),
                                     layout="owner" if layout == "owner" else "committee",
-                                    waves=3, force_pipeline=True, deadline_s=30.0)
+                                    waves=3, force_pipeline=True, deadline_s=30.0,
+                                    strict_liveness=layout == "strict")
         # key custody: only the hosted clerks' secret keys (+ the recipient's on rank 0)
         if layout != "owner":
             from sda_amd.parallel.routing import hosted_clerks
@@ -80,7 +81,10 @@ def _worker(rank, world, port, name, layout, q):
                                                # must not wrap (pipelined waves, world 1 and 2)
                                                (1, "bigmod", "committee"),
                                                (2, "bigmod", "committee"),
-                                               (3, "fullmask", "stream")])
+                                               (3, "fullmask", "stream"),
+                                               # liveness flags posted only once the GPU has
+                                               # finished the work in front of the stage
+                                               (2, "pss", "strict"), (3, "additive2", "strict")])
 def test_distributed_device_ranks_one_gpu(cuda, world, name, layout):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
