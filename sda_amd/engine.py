@@ -498,7 +498,7 @@ class DeviceAggregator:
         elif isinstance(spec.masking, ChaChaMask):
             mask_arena = Arena.empty(P, spec.masking.seed_words, 0, dev)
         kidx_clerk = self._kidx_clerk(P)
-        kidx_rcpt_p = torch.full((P,), n, dtype=torch.int32, device=dev)
+        kidx_rcpt_p = self._kidx_recipient(P) if mask_arena is not None else None
 
         # ---- side stream: key agreement (data independent)
         gate = self._gate_token()
@@ -697,6 +697,13 @@ class DeviceAggregator:
         if P not in cache:
             cache[P] = torch.arange(self.n, dtype=torch.int32,
                                     device=self.device).repeat_interleave(P)
+        return cache[P]
+
+    def _kidx_recipient(self, P: int) -> torch.Tensor:
+        """P times the recipient's key index (the participants' mask boxes), cached."""
+        cache = self.__dict__.setdefault("_kidx_rcpt_cache", {})
+        if P not in cache:
+            cache[P] = torch.full((P,), self.n, dtype=torch.int32, device=self.device)
         return cache[P]
 
     def _open_keys(self, arena, kidx, live, P, err):
