@@ -103,6 +103,9 @@ def main(argv):
         rd = f.get("FETCH_SIZE", 0) * calls * 1024 / 1e9
         wr = w.get("WRITE_SIZE", 0) * calls * 1024 / 1e9
         model = MODEL_GB.get(k)
+        if model is None:  # template arguments added since (e.g. the tile's code length)
+            model = next((v for name, v in MODEL_GB.items()
+                          if k.startswith(name.rstrip(">") + ",")), None)
         mtxt = f"{model[0]:5.2f}+{model[1]:4.2f}" if model else ""
         moved = sum(model) if model else rd + wr
         print(f"{k:44s} {calls:6.1f} {ms:7.3f} {valu * 64 / CIPHERTEXT_BYTES:10.1f} "
