@@ -102,11 +102,12 @@ def parse():
     ap.add_argument("--waves", type=lambda v: v if v == "taper" else int(v), default=0,
                     help="committee layout: participant waves the exchange is pipelined over. "
                          "A count, or 'taper' (six waves of 1/16, 3/16, 4/16, 4/16, 3/16, 1/16 of the "
-                         "participants). 0 (default): with N > 1, 2 / 4 / 8 / taper are timed for "
-                         "two untimed rounds each before the warm-up and the fastest is used (more "
-                         "waves start the all-to-all earlier and shorten the exposed last wave, "
-                         "fewer waves keep the grids large: which wins depends on the xGMI rate "
-                         "RCCL reaches); 4 on a single rank")
+                         "participants). 0 (default): with N > 1, 1 / 2 / 4 / 8 / taper are timed for "
+                         "three untimed rounds each before the warm-up and the fastest is used "
+                         "(more waves start the all-to-all earlier and shorten the exposed last "
+                         "wave, fewer waves keep the grids large -- one wave exposes the whole "
+                         "exchange but costs a rank 0.4 ms less compute than four: which wins "
+                         "depends on the xGMI rate RCCL reaches); 4 on a single rank")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the distributed engine even on one rank (measures its overhead)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -269,7 +270,7 @@ def main():
         if not args.waves and world > 1 and args.layout == "committee":
             # untimed: pick the pipeline depth on this node's measured exchange rate
             # (every rank takes the same decision: the times are max-reduced)
-            for w in (2, 4, 8, "taper"):
+            for w in (1, 2, 4, 8, "taper"):
                 agg.set_waves(w)
                 agg.run_round(secrets, check=True)
                 best = float("inf")
