@@ -256,6 +256,7 @@ PYBIND11_MODULE(_sda_gpu, m) {
   m.def("set_decode_lean", &set_decode_lean);
   m.def("set_decode_swz", &set_decode_swz);
   m.def("set_decode_long", &set_decode_long);
+  m.def("set_encode_tile2", &set_encode_tile2);
   m.def("set_seal_many", &set_seal_many);
   m.def("x25519_base", [](int N, uintptr_t sc, uintptr_t out, uintptr_t stream) {
     launch_x25519_base(N, P<const uint32_t>(sc), P<uint32_t>(out), S(stream));

@@ -240,6 +240,7 @@ void set_decode_swz(int mode);
 // lean decode-sum of three- and four-byte fields: 1 walks values (one LDS add per value),
 // 0 adds byte by byte like the short-code kernel, -1 (default) the former for three-byte fields
 void set_decode_long(int mode);
+void set_encode_tile2(int on);
 // Column sums mod m: out[g][l] = sum_r vals[g][r][l] mod m.
 void launch_colsum(int G, int R, int L, uint32_t m, int value_bytes, const void* vals,
                    uint32_t* out, hipStream_t s);

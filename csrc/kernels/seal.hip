@@ -94,9 +94,9 @@ SDA_DEV void load_values(uint32_t (&v)[kValuesPerLane], const VT* src, int e0, i
 //   row value  = (sum_pos u_pos W(pos) + row constant + pad bits of the owned blocks)
 //   chunk part = sum_i row value_i * r^(16 - i)     (relative to the chunk's end, as
 //                                                    k_mac_chunks' middle chunks are)
-// kMaxB: the longest code the caller's values can have (u8 / u16 storage: 3; u32: 3 for
-// values below 2^20, 4 below 2^27, else 5). It sizes the tile's LDS -- 24 / 32 / 40 KB,
-// i.e. six / four / three workgroups a CU; the issue-bound kernel ran at 57 % of its
+// kMaxB: the longest code the caller's values can have (u8 / u16 storage: 3, or 2 for
+// 16-bit values below 2^13; u32: 3 for values below 2^20, 4 below 2^27, else 5). It sizes
+// the tile's LDS -- 16 / 24 / 32 / 40 KB, i.e. eight / six / four / three workgroups a CU; the issue-bound kernel ran at 57 % of its
 // VALU peak with three -- and a value past the bound (a caller's error: the slots of
 // the arena are sized by the same bound) is encoded as zero rather than overrun it.
 template <typename VT, bool MAC, int kMaxB>
@@ -105,7 +105,8 @@ __global__ void __launch_bounds__(kBlock)
                      const MsgKey* __restrict__ keys, uint8_t* __restrict__ ct, uint64_t stride,
                      const uint32_t* __restrict__ pows, const uint32_t* __restrict__ pt_len,
                      uint32_t* __restrict__ partials, int K) {
-  static_assert(kMaxB >= 3 && kMaxB <= 5 && (sizeof(VT) > 2 || kMaxB == 3), "code length bound");
+  static_assert(kMaxB >= 2 && kMaxB <= 5 && (sizeof(VT) > 2 || kMaxB <= 3) &&
+                (kMaxB > 2 || (sizeof(VT) == 2 && !MAC)), "code length bound");
   constexpr uint32_t kBound = kMaxB == 5 ? 0xffffffffu : (1u << (7 * kMaxB - 1)) - 1u;  // largest value
   // Five-byte codes: the tile goes through LDS in two passes, the first two waves' values and
   // then the other two's (all four waves on the keystream and the stores of either pass), so
@@ -194,6 +195,11 @@ __global__ void __launch_bounds__(kBlock)
       }
 #pragma unroll
       for (int k = 0; k < kValuesPerLane / 2; ++k) orp |= pr[k];
+    }
+    if (kMaxB == 2 && (orp & 0xe000e000u) != 0u) {  // past the bound: never with canonical values
+#pragma unroll
+      for (int k = 0; k < kValuesPerLane / 2; ++k) pr[k] = 0;
+      orp = 0;
     }
     fast = full && (orp & 0xe000e000u) == 0u;
     if (fast) {
@@ -1219,6 +1225,10 @@ void launch_segscan(int M, int T, uint32_t* data, uint32_t* totals, uint32_t exp
   hipLaunchKernelGGL(k_segscan, dim3(M), dim3(kBlock), 0, s, T, data, totals, expect, err);
 }
 
+// 16-bit values below 2^13 (codes of at most two bytes) in a tile sized for them
+static int g_encode_tile2 = 1;
+void set_encode_tile2(int on) { g_encode_tile2 = on; }
+
 template <typename VT, int kMaxB>
 static void launch_encode_t(int M, int L, const void* vals, const uint32_t* tile_off,
                             const MsgKey* keys, uint8_t* ct, uint64_t stride, const uint32_t* pows,
@@ -1239,6 +1249,8 @@ void launch_encode_encrypt(int M, int L, int value_bytes, const void* vals,
   if (M <= 0 || L <= 0) return;
   if (value_bytes == 1)
     launch_encode_t<uint8_t, 3>(M, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
+  else if (value_bytes == 2 && max_code_bytes <= 2 && g_encode_tile2 && !(pows && pt_len && partials))
+    launch_encode_t<uint16_t, 2>(M, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
   else if (value_bytes == 2)
     launch_encode_t<uint16_t, 3>(M, L, vals, tile_off, keys, ct, stride, pows, pt_len, partials, K, s);
   else if (max_code_bytes <= 3)
